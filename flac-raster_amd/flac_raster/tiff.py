@@ -1,0 +1,292 @@
+"""Minimal GeoTIFF reader/writer (numpy only) standing in for the rasterio calls on the encode path.
+
+The reference reads rasters with ``rasterio.open(...).read()`` (``converter.py:73-79``) and
+``src.read(window=...)`` (``cli.py:559``, ``spatial_encoder.py:205-206``) and writes tile GeoTIFFs
+(``cli.py:577-591``).  rasterio/GDAL are not part of this image, so this module implements the
+subset the encode path needs:
+
+* baseline TIFF + BigTIFF, II/MM byte order, strips or tiles, PlanarConfiguration 1 or 2,
+  Compression 1 (none), 8 (Adobe deflate), 32946 (deflate); Predictor 1/2 for integers;
+* SampleFormat uint / int / IEEE float, 8/16/32/64 bits;
+* GeoTIFF ModelPixelScale + ModelTiepoint or ModelTransformation -> affine transform
+  (GDAL order ``(a, b, c, d, e, f)`` as ``list(rasterio.Affine)[:6]``), GeoKeyDirectory -> ``EPSG:n``.
+
+Arrays are returned band-planar ``(bands, height, width)`` like ``rasterio.read()``.
+"""
+
+from __future__ import annotations
+
+import struct
+import zlib
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+_TYPE_SIZES = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 6: 1, 7: 1, 8: 2, 9: 4, 10: 8, 11: 4, 12: 8, 16: 8, 17: 8, 18: 8}
+_TYPE_FMT = {1: "B", 2: "c", 3: "H", 4: "I", 5: "II", 6: "b", 7: "B", 8: "h", 9: "i", 10: "ii", 11: "f",
+             12: "d", 16: "Q", 17: "q", 18: "Q"}
+
+
+@dataclass
+class RasterInfo:
+    width: int
+    height: int
+    count: int
+    dtype: np.dtype
+    transform: tuple = (1.0, 0.0, 0.0, 0.0, 1.0, 0.0)  # a, b, c, d, e, f
+    crs: Optional[str] = None
+    nodata: Optional[float] = None
+    tags: dict = field(default_factory=dict)
+
+    @property
+    def bounds(self):
+        a, b, c, d, e, f = self.transform
+        xs = [c, c + a * self.width]
+        ys = [f, f + e * self.height]
+        return (min(xs), min(ys), max(xs), max(ys))  # left, bottom, right, top
+
+    def window_transform(self, col_off: int, row_off: int):
+        a, b, c, d, e, f = self.transform
+        return (a, b, c + a * col_off + b * row_off, d, e, f + d * col_off + e * row_off)
+
+
+def _dtype_from(fmt: int, bits: int) -> np.dtype:
+    kind = {1: "u", 2: "i", 3: "f"}.get(fmt, "u")
+    return np.dtype(f"{kind}{bits // 8}")
+
+
+class GeoTIFF:
+    """Read-only GeoTIFF.  ``read()`` -> (bands, H, W); ``read_window(r, c, h, w)``."""
+
+    def __init__(self, path):
+        self.path = Path(path)
+        self._buf = self.path.read_bytes()
+        b = self._buf
+        if b[:2] == b"II":
+            self.bo = "<"
+        elif b[:2] == b"MM":
+            self.bo = ">"
+        else:
+            raise ValueError(f"not a TIFF: {path}")
+        magic = struct.unpack(self.bo + "H", b[2:4])[0]
+        self.big = magic == 43
+        if self.big:
+            off = struct.unpack(self.bo + "Q", b[8:16])[0]
+        elif magic == 42:
+            off = struct.unpack(self.bo + "I", b[4:8])[0]
+        else:
+            raise ValueError("bad TIFF magic")
+        self.tags = self._read_ifd(off)
+        t = self.tags
+        W, H = int(t[256][0]), int(t[257][0])
+        spp = int(t.get(277, [1])[0])
+        bits = t.get(258, [8] * spp)
+        fmt = int(t.get(339, [1])[0])
+        self.dtype = _dtype_from(fmt, int(bits[0])).newbyteorder(self.bo)
+        self.planar = int(t.get(284, [1])[0])
+        self.compression = int(t.get(259, [1])[0])
+        self.predictor = int(t.get(317, [1])[0])
+        transform = (1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+        if 34264 in t:
+            m = t[34264]
+            transform = (m[0], m[1], m[3], m[4], m[5], m[7])
+        elif 33550 in t and 33922 in t:
+            sx, sy = t[33550][0], t[33550][1]
+            tp = t[33922]
+            i, j, x, y = tp[0], tp[1], tp[3], tp[4]
+            transform = (sx, 0.0, x - i * sx, 0.0, -sy, y + j * sy)
+        crs = None
+        if 34735 in t:
+            keys = t[34735]
+            for k in range(4, len(keys), 4):
+                kid, loc, cnt, val = keys[k:k + 4]
+                if kid in (2048, 3072) and loc == 0:
+                    crs = f"EPSG:{val}"
+                    if kid == 3072:
+                        break
+        nodata = None
+        if 42113 in t:
+            try:
+                nodata = float(t[42113].strip("\x00"))
+            except ValueError:
+                nodata = None
+        self.info = RasterInfo(W, H, spp, np.dtype(self.dtype.newbyteorder("=")), transform, crs, nodata, {})
+        self._data = None
+
+    # -- IFD parsing
+    def _read_ifd(self, off: int) -> dict:
+        b, bo = self._buf, self.bo
+        if self.big:
+            n = struct.unpack(bo + "Q", b[off:off + 8])[0]
+            esz, p, inl = 20, off + 8, 8
+        else:
+            n = struct.unpack(bo + "H", b[off:off + 2])[0]
+            esz, p, inl = 12, off + 2, 4
+        tags = {}
+        for i in range(n):
+            e = b[p + i * esz:p + (i + 1) * esz]
+            tag, typ = struct.unpack(bo + "HH", e[:4])
+            if self.big:
+                cnt = struct.unpack(bo + "Q", e[4:12])[0]
+                raw = e[12:20]
+            else:
+                cnt = struct.unpack(bo + "I", e[4:8])[0]
+                raw = e[8:12]
+            size = _TYPE_SIZES.get(typ, 1) * cnt
+            if size > inl:
+                vo = struct.unpack(bo + ("Q" if self.big else "I"), raw)[0]
+                data = b[vo:vo + size]
+            else:
+                data = raw[:size]
+            if typ == 2:
+                tags[tag] = data.decode("latin-1")
+            elif typ in (5, 10):
+                v = struct.unpack(bo + _TYPE_FMT[typ][0] * (2 * cnt), data)
+                tags[tag] = [v[2 * k] / v[2 * k + 1] if v[2 * k + 1] else 0.0 for k in range(cnt)]
+            else:
+                tags[tag] = list(struct.unpack(bo + _TYPE_FMT.get(typ, "B") * cnt, data))
+        return tags
+
+    def _decode_chunk(self, raw: bytes) -> bytes:
+        if self.compression == 1:
+            return raw
+        if self.compression in (8, 32946):
+            return zlib.decompress(raw)
+        raise NotImplementedError(f"TIFF compression {self.compression} not supported")
+
+    def read(self) -> np.ndarray:
+        """All bands, (count, H, W) native-endian -- rasterio ``read()`` equivalent."""
+        if self._data is not None:
+            return self._data
+        t, info = self.tags, self.info
+        W, H, S = info.width, info.height, info.count
+        dt = self.dtype
+        out = np.empty((S, H, W), dtype=dt.newbyteorder("="))
+        tiled = 322 in t
+        offs = t[324] if tiled else t[273]
+        cnts = t[325] if tiled else t[279]
+        if tiled:
+            tw, th = int(t[322][0]), int(t[323][0])
+        else:
+            tw, th = W, int(t.get(278, [H])[0])
+        nx = (W + tw - 1) // tw
+        ny = (H + th - 1) // th
+        per_plane = nx * ny
+        planes = S if self.planar == 2 else 1
+        spc = 1 if self.planar == 2 else S
+        for pl in range(planes):
+            for cy in range(ny):
+                for cx in range(nx):
+                    idx = pl * per_plane + cy * nx + cx
+                    raw = self._buf[offs[idx]:offs[idx] + cnts[idx]]
+                    dec = self._decode_chunk(raw)
+                    rows = th if tiled else min(th, H - cy * th)
+                    arr = np.frombuffer(dec, dtype=dt, count=rows * tw * spc).reshape(rows, tw, spc)
+                    if self.predictor == 2:
+                        arr = np.cumsum(arr, axis=1, dtype=arr.dtype)
+                    r0, c0 = cy * th, cx * tw
+                    r1, c1 = min(r0 + rows, H), min(c0 + tw, W)
+                    blk = arr[: r1 - r0, : c1 - c0, :]
+                    if self.planar == 2:
+                        out[pl, r0:r1, c0:c1] = blk[:, :, 0]
+                    else:
+                        out[:, r0:r1, c0:c1] = np.moveaxis(blk, 2, 0)
+        self._data = out
+        return out
+
+    def read_window(self, row_off: int, col_off: int, height: int, width: int) -> np.ndarray:
+        return self.read()[:, row_off:row_off + height, col_off:col_off + width]
+
+
+def read_geotiff(path):
+    g = GeoTIFF(path)
+    return g.read(), g.info
+
+
+def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = None, nodata=None):
+    """Write an uncompressed, pixel-interleaved, single-strip-per-row-block little-endian GeoTIFF."""
+    data = np.asarray(data)
+    if data.ndim == 2:
+        data = data[None]
+    S, H, W = data.shape
+    dt = data.dtype
+    fmt = 3 if dt.kind == "f" else (2 if dt.kind == "i" else 1)
+    bits = dt.itemsize * 8
+    pix = np.ascontiguousarray(np.moveaxis(data, 0, 2)).astype(dt.newbyteorder("<"), copy=False)
+    rows_per_strip = max(1, min(H, (1 << 16) // max(1, W * S * dt.itemsize)))
+    strips = [pix[r:r + rows_per_strip].tobytes() for r in range(0, H, rows_per_strip)]
+    entries = []  # (tag, type, values)
+    entries.append((256, 3 if W < 65536 else 4, [W]))
+    entries.append((257, 3 if H < 65536 else 4, [H]))
+    entries.append((258, 3, [bits] * S))
+    entries.append((259, 3, [1]))
+    entries.append((262, 3, [2 if S == 3 and dt == np.uint8 else 1]))
+    entries.append((273, 4, [0] * len(strips)))
+    entries.append((277, 3, [S]))
+    entries.append((278, 4, [rows_per_strip]))
+    entries.append((279, 4, [len(s) for s in strips]))
+    entries.append((284, 3, [1]))
+    entries.append((339, 3, [fmt] * S))
+    if transform is not None:
+        a, b, c, d, e, f = [float(v) for v in list(transform)[:6]]
+        if b == 0.0 and d == 0.0:
+            entries.append((33550, 12, [a, -e, 0.0]))
+            entries.append((33922, 12, [0.0, 0.0, 0.0, c, f, 0.0]))
+        else:
+            entries.append((34264, 12, [a, b, 0.0, c, d, e, 0.0, f, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0]))
+    if crs and str(crs).upper().startswith("EPSG:"):
+        code = int(str(crs).split(":")[1])
+        geographic = 4000 <= code < 5000
+        keys = [1, 1, 0, 3, 1024, 0, 1, 2 if geographic else 1, 1025, 0, 1, 1,
+                2048 if geographic else 3072, 0, 1, code]
+        entries.append((34735, 3, keys))
+    if nodata is not None:
+        entries.append((42113, 2, (str(nodata) + "\x00").encode("latin-1")))
+    entries.sort(key=lambda x: x[0])
+    # layout: header(8) | IFD | external values | strips
+    n = len(entries)
+    ifd_size = 2 + 12 * n + 4
+    ext = bytearray()
+    ext_base = 8 + ifd_size
+    packed = []
+    fmtmap = {3: "H", 4: "I", 12: "d"}
+    for tag, typ, vals in entries:
+        if typ == 2:
+            raw = bytes(vals)
+            cnt = len(raw)
+        else:
+            raw = struct.pack("<" + fmtmap[typ] * len(vals), *vals)
+            cnt = len(vals)
+        packed.append([tag, typ, cnt, raw])
+    # strip offsets need final positions: compute external area first with placeholder offsets
+    for it in packed:
+        if len(it[3]) > 4:
+            it.append(ext_base + len(ext))
+            ext += it[3]
+            if len(ext) % 2:
+                ext += b"\x00"
+        else:
+            it.append(None)
+    strip_base = ext_base + len(ext)
+    offsets, pos = [], strip_base
+    for s in strips:
+        offsets.append(pos)
+        pos += len(s)
+    for it in packed:  # patch StripOffsets
+        if it[0] == 273:
+            raw = struct.pack("<" + "I" * len(offsets), *offsets)
+            it[3] = raw
+            if it[4] is not None:
+                ext[it[4] - ext_base:it[4] - ext_base + len(raw)] = raw
+    out = bytearray(b"II*\x00" + struct.pack("<I", 8))
+    out += struct.pack("<H", n)
+    for tag, typ, cnt, raw, loc in packed:
+        out += struct.pack("<HHI", tag, typ, cnt)
+        out += struct.pack("<I", loc) if loc is not None else raw.ljust(4, b"\x00")
+    out += struct.pack("<I", 0)
+    out += ext
+    for s in strips:
+        out += s
+    Path(path).write_bytes(bytes(out))

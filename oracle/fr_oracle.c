@@ -1,0 +1,1036 @@
+/*
+ * fr_oracle.c -- CPU ORACLE for the flac-raster MI355X encode path.
+ *
+ *   *** TEST INFRASTRUCTURE ONLY ***
+ *   Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ *   library, and only as the checker / CPU baseline.  The product path
+ *   (flac-raster_amd/, libflac_raster_amd.so) never links, loads or falls back to it.
+ *
+ * What it restates (reference = yharby/flac-raster @ 2026-02-27, read-only at /root/reference):
+ *   - normalize_to_audio / calculate_audio_params   src/flac_raster/normalization.py:78-202
+ *     (numpy float64 op order: ((2.0*(x-mn))/R)-1.0, clip[-1,1], NaN->0, *scale, trunc cast)
+ *   - the band interleave                           src/flac_raster/converter.py:99-110
+ *   - the libFLAC 1.4.3 encode that pyflac.StreamEncoder drives
+ *                                                   src/flac_raster/converter.py:139-154,
+ *                                                   src/flac_raster/spatial_encoder.py:291-304,
+ *                                                   docs/sonos-pyflac.txt:1968-2014 (process/finish)
+ *     libFLAC itself is a third-party dependency (pyflac 3.0.0 -> libFLAC 1.4.3, uv.lock:844-846)
+ *     that is NOT present in /root/reference; its sources are absent.  What is restated here
+ *     is the published FLAC format (RFC 9639; constants at docs/sonos-pyflac.txt:3488-3546),
+ *     libFLAC's compression-level table (docs/sonos-pyflac.txt:6926-6934) and its published
+ *     analysis algorithm (tukey apodization -> autocorrelation -> Levinson-Durbin -> qlp
+ *     quantisation -> fixed/LPC residual -> partitioned Rice).  Model *selection* is this
+ *     project's deterministic rule ("FRA-1") so that the GPU encoder can
+ *     be checked byte-for-byte against this file; libFLAC's own byte stream is not
+ *     reproducible without its sources.  Parity with the reference is pinned by
+ *       (1) decoding the committed libFLAC golden test_data/sample_rgb.flac bit-exactly to
+ *           normalize_to_audio(sample_rgb.tif) (fixtures in tests/golden/), and
+ *       (2) every encoded stream decoding bit-exactly to its input, and
+ *       (3) compressed size vs the golden's 178,857 frame bytes.
+ *   - a complete FLAC decoder (CONSTANT/VERBATIM/FIXED/LPC, RICE/RICE2/escape, all channel
+ *     assignments, 4..32 bps, CRC-8/CRC-16 checked) used as the round-trip verifier.
+ *
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORA_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ dtype codes */
+enum { DT_U8 = 0, DT_I8, DT_U16, DT_I16, DT_U32, DT_I32, DT_F32, DT_F64 };
+
+static double load_as_f64(const void *p, int dt, size_t i) {
+  switch (dt) {
+  case DT_U8: return (double)((const uint8_t *)p)[i];
+  case DT_I8: return (double)((const int8_t *)p)[i];
+  case DT_U16: return (double)((const uint16_t *)p)[i];
+  case DT_I16: return (double)((const int16_t *)p)[i];
+  case DT_U32: return (double)((const uint32_t *)p)[i];
+  case DT_I32: return (double)((const int32_t *)p)[i];
+  case DT_F32: return (double)((const float *)p)[i];
+  default: return ((const double *)p)[i];
+  }
+}
+
+/* ================================================================== normalization
+ * normalization.py:148-151: mn = float(np.nanmin(data)), mx = float(np.nanmax(data)).
+ * All-NaN -> both NaN.  Returns the count of non-NaN values. */
+ORA_API int64_t ora_minmax(const void *data, int dt, size_t n, double *mn, double *mx) {
+  double lo = NAN, hi = NAN;
+  int64_t cnt = 0;
+  for (size_t i = 0; i < n; i++) {
+    double v = load_as_f64(data, dt, i);
+    if (v != v) continue;
+    if (cnt == 0 || v < lo) lo = v;
+    if (cnt == 0 || v > hi) hi = v;
+    cnt++;
+  }
+  *mn = lo;
+  *mx = hi;
+  return cnt;
+}
+
+/* normalization.py:154-187 (bps 16 -> int16 out, bps 24 -> int32 out). */
+ORA_API int ora_normalize(const void *data, int dt, size_t n, int bps, double mn, double mx, void *out) {
+  double range;
+  if (mx <= mn) range = 1.0;          /* :154-157 (NaN compares false -> range = NaN) */
+  else range = mx - mn;               /* :159 */
+  double scale = (bps == 16) ? 32767.0 : (bps == 24 ? 8388607.0 : 2147483647.0);
+  for (size_t i = 0; i < n; i++) {
+    double x = load_as_f64(data, dt, i);
+    double t = x - mn;                /* data_float - data_min */
+    t = 2.0 * t;                      /* 2.0 * (...) */
+    t = t / range;                    /* / data_range */
+    t = t - 1.0;                      /* - 1.0 */
+    if (t < -1.0) t = -1.0;           /* np.clip keeps NaN */
+    else if (t > 1.0) t = 1.0;
+    if (t != t) t = 0.0;              /* NaN -> 0 (:171-175) */
+    t = t * scale;
+    if (bps == 16) ((int16_t *)out)[i] = (int16_t)t;   /* astype(int16): trunc */
+    else ((int32_t *)out)[i] = (int32_t)t;             /* astype(int32): trunc */
+  }
+  return 0;
+}
+
+/* normalization.py:108-120 */
+ORA_API int ora_sample_rate_for_pixels(int64_t px) {
+  if (px < 1000000) return 44100;
+  if (px < 10000000) return 48000;
+  if (px < 100000000) return 96000;
+  return 192000;
+}
+
+/* ================================================================== CRCs (RFC 9639 9.1.8 / 9.3) */
+static uint8_t crc8_tab[256];
+static uint16_t crc16_tab[256];
+static int crc_init_done = 0;
+static void crc_init(void) {
+  if (crc_init_done) return;
+  for (int i = 0; i < 256; i++) {
+    unsigned c = (unsigned)i;
+    for (int b = 0; b < 8; b++) c = (c & 0x80) ? ((c << 1) ^ 0x07) : (c << 1);
+    crc8_tab[i] = (uint8_t)c;
+    unsigned d = (unsigned)i << 8;
+    for (int b = 0; b < 8; b++) d = (d & 0x8000) ? ((d << 1) ^ 0x8005) : (d << 1);
+    crc16_tab[i] = (uint16_t)d;
+  }
+  crc_init_done = 1;
+}
+ORA_API unsigned ora_crc8(const uint8_t *p, size_t n) {
+  crc_init();
+  unsigned c = 0;
+  for (size_t i = 0; i < n; i++) c = crc8_tab[(c ^ p[i]) & 0xFF];
+  return c;
+}
+ORA_API unsigned ora_crc16(const uint8_t *p, size_t n) {
+  crc_init();
+  unsigned c = 0;
+  for (size_t i = 0; i < n; i++) c = ((c << 8) ^ crc16_tab[((c >> 8) ^ p[i]) & 0xFF]) & 0xFFFF;
+  return c;
+}
+
+/* ================================================================== bit writer (MSB first) */
+typedef struct {
+  uint8_t *buf;
+  size_t cap;
+  uint64_t bits;
+} bw_t;
+
+static void bw_reserve(bw_t *w, uint64_t extra_bits) {
+  size_t need = (size_t)((w->bits + extra_bits + 7) / 8) + 8;
+  if (need <= w->cap) return;
+  size_t nc = w->cap ? w->cap : 4096;
+  while (nc < need) nc *= 2;
+  uint8_t *nb = (uint8_t *)realloc(w->buf, nc);
+  memset(nb + w->cap, 0, nc - w->cap);
+  w->buf = nb;
+  w->cap = nc;
+}
+static void bw_put(bw_t *w, uint64_t v, int nb) { /* nb <= 64 */
+  if (nb <= 0) return;
+  bw_reserve(w, (uint64_t)nb);
+  for (int i = nb - 1; i >= 0; i--) {
+    if ((v >> i) & 1) w->buf[w->bits >> 3] |= (uint8_t)(0x80u >> (w->bits & 7));
+    w->bits++;
+  }
+}
+static void bw_zeros(bw_t *w, uint64_t nb) {
+  bw_reserve(w, nb);
+  w->bits += nb;
+}
+static void bw_align(bw_t *w) {
+  uint64_t r = w->bits & 7;
+  if (r) bw_zeros(w, 8 - r);
+}
+
+/* ================================================================== level table
+ * docs/sonos-pyflac.txt:6926-6934 (libFLAC 1.4.3 FLAC__stream_encoder_set_compression_level).
+ * nwin: 1 = tukey(0.5); n>1 = subdivide into n (full tukey + partial tukeys over 1/m, m=2..n). */
+typedef struct {
+  int max_lpc;
+  int max_porder;
+  int nsub;     /* 0 = no LPC, 1 = tukey(0.5), 2/3 = subdivide_tukey(2/3) */
+  int stereo;   /* mid-side tried for C == 2 (not applied in FRA-1: independent channels) */
+} level_cfg;
+static const level_cfg LEVELS[9] = {
+    {0, 3, 0, 0}, {0, 3, 0, 1}, {0, 3, 0, 1}, {6, 4, 1, 0}, {8, 4, 1, 1},
+    {8, 5, 1, 1}, {8, 6, 2, 1}, {12, 6, 2, 1}, {12, 6, 3, 1}};
+
+/* qlp coefficient precision, libFLAC "auto" rule (qlp_coeff_precision == 0):
+ * bps <= 16 by blocksize ladder, > 16 -> 13/14/15. */
+static int qlp_precision(int bps, int bs) {
+  if (bps < 16) { int p = 2 + bps / 2; return p < 5 ? 5 : p; }
+  if (bps == 16) {
+    if (bs <= 192) return 7;
+    if (bs <= 384) return 8;
+    if (bs <= 576) return 9;
+    if (bs <= 1152) return 10;
+    if (bs <= 2304) return 11;
+    if (bs <= 4608) return 12;
+    return 13;
+  }
+  if (bs <= 384) return 13;
+  if (bs <= 1152) return 14;
+  return 15;
+}
+
+/* ================================================================== windows (host-side tables)
+ * tukey(p) exactly as DESIGN.md 3.4: Np = (int)(p/2*N) - 1; cosine tapers of length Np+1. */
+ORA_API void ora_window_tukey(float *w, int N, double p) {
+  for (int i = 0; i < N; i++) w[i] = 1.0f;
+  int Np = (int)(p / 2.0 * (double)N) - 1;
+  if (Np > 0) {
+    for (int n = 0; n <= Np; n++) {
+      w[n] = (float)(0.5 - 0.5 * cos(M_PI * (double)n / (double)Np));
+      w[N - Np - 1 + n] = (float)(0.5 - 0.5 * cos(M_PI * (double)(n + Np) / (double)Np));
+    }
+  }
+}
+/* window set for a block of N samples at subdivision nsub: index 0 = full tukey(0.5);
+ * then for m = 2..nsub, parts j = 0..m-1: tukey(0.5) over [j*N/m, (j+1)*N/m), zero elsewhere. */
+ORA_API int ora_num_windows(int nsub) {
+  int c = nsub > 0 ? 1 : 0;
+  for (int m = 2; m <= nsub; m++) c += m;
+  return c;
+}
+ORA_API void ora_window_set(float *w /* nwin*N */, int N, int nsub) {
+  if (nsub <= 0) return;
+  ora_window_tukey(w, N, 0.5);
+  int idx = 1;
+  for (int m = 2; m <= nsub; m++) {
+    for (int j = 0; j < m; j++, idx++) {
+      float *o = w + (size_t)idx * N;
+      int a = (int)((int64_t)j * N / m), b = (int)((int64_t)(j + 1) * N / m);
+      for (int i = 0; i < N; i++) o[i] = 0.0f;
+      if (b - a > 0) ora_window_tukey(o + a, b - a, 0.5);
+    }
+  }
+}
+
+/* ================================================================== analysis primitives */
+
+/* Autocorrelation, FRA-1 fixed reduction order: 16-sample chunks summed sequentially
+ * (acc starts at +0.0, products of two floats are exact in double), 256 chunk partials
+ * (zero padded) reduced by a pairwise tree: stride 1,2,4,...,128, P[j] = P[j] + P[j+s]. */
+ORA_API void ora_autocorr(const float *wf, int n, int maxlag, double *autoc) {
+  double P[256];
+  for (int l = 0; l <= maxlag; l++) {
+    for (int j = 0; j < 256; j++) {
+      double acc = 0.0;
+      for (int i = 16 * j; i < 16 * j + 16; i++) {
+        if (i + l < n) acc = acc + (double)wf[i] * (double)wf[i + l];
+      }
+      P[j] = acc;
+    }
+    for (int s = 1; s < 256; s <<= 1)
+      for (int j = 0; j < 256; j += 2 * s) P[j] = P[j] + P[j + s];
+    autoc[l] = P[0];
+  }
+}
+
+/* Levinson-Durbin.  lp[o-1][j], j<o = predictor coefficients for order o,
+ * err[o-1] = prediction error.  Returns the number of valid orders (stops when err <= 0). */
+ORA_API int ora_levinson(const double *autoc, int max_order, double *lp /* max_order*32 */, double *err_out) {
+  double lpc[32];
+  double err = autoc[0];
+  int i;
+  for (i = 0; i < max_order; i++) {
+    double r = -autoc[i + 1];
+    for (int j = 0; j < i; j++) r = r - lpc[j] * autoc[i - j];
+    r = r / err;
+    lpc[i] = r;
+    int j;
+    for (j = 0; j < (i >> 1); j++) {
+      double tmp = lpc[j];
+      lpc[j] = lpc[j] + r * lpc[i - 1 - j];
+      lpc[i - 1 - j] = lpc[i - 1 - j] + r * tmp;
+    }
+    if (i & 1) lpc[j] = lpc[j] + lpc[j] * r;
+    err = err * (1.0 - r * r);
+    for (j = 0; j <= i; j++) lp[i * 32 + j] = -lpc[j];
+    err_out[i] = err;
+    if (err > 0.0) continue;
+    return err == 0.0 ? i + 1 : i; /* perfect predictor keeps order i+1; err<0 or NaN drops it */
+  }
+  return max_order;
+}
+
+/* round half away from zero, exact */
+static double rnd_half_away(double x) {
+  double t = trunc(x);
+  double d = x - t;
+  if (d >= 0.5) t = t + 1.0;
+  else if (d <= -0.5) t = t - 1.0;
+  return t;
+}
+
+/* qlp quantisation with error feedback.  Returns 0 on success, -1 if the
+ * coefficients cannot be represented (cmax too large or zero). */
+ORA_API int ora_quantize(const double *lp, int order, int precision, int32_t *q, int *shift_out) {
+  double cmax = 0.0;
+  for (int j = 0; j < order; j++) {
+    double a = fabs(lp[j]);
+    if (a > cmax) cmax = a;
+  }
+  if (!(cmax > 0.0)) return -1;
+  int e;
+  (void)frexp(cmax, &e); /* cmax < 2^e */
+  int shift = precision - 1 - e;
+  if (shift > 15) shift = 15;
+  if (shift < 0) return -1;
+  int32_t qmax = (1 << (precision - 1)) - 1, qmin = -(1 << (precision - 1));
+  double errf = 0.0;
+  for (int j = 0; j < order; j++) {
+    errf = errf + ldexp(lp[j], shift);
+    double qd = rnd_half_away(errf);
+    int32_t qi = (int32_t)qd;
+    if (qi > qmax) qi = qmax;
+    if (qi < qmin) qi = qmin;
+    errf = errf - (double)qi;
+    q[j] = qi;
+  }
+  *shift_out = shift;
+  return 0;
+}
+
+static int bitlen_u64(uint64_t v) { int b = 0; while (v) { b++; v >>= 1; } return b; }
+
+/* deterministic log2 (frexp + atanh series), DESIGN.md 3.7 */
+ORA_API double ora_det_log2(double x) {
+  int e;
+  double m = frexp(x, &e);
+  m = m * 2.0;
+  e = e - 1;
+  double t = (m - 1.0) / (m + 1.0);
+  double t2 = t * t;
+  double sum = 0.0, p = t;
+  for (int k = 0; k < 12; k++) {
+    sum = sum + p / (double)(2 * k + 1);
+    p = p * t2;
+  }
+  return (double)e + 2.0 * sum * 1.4426950408889634;
+}
+
+/* LPC order choice for non-primary windows from LD error (libFLAC-style expected bits). */
+static int best_order_by_error(const double *err, int norders, int n, int overhead_per_order) {
+  double best = 0.0;
+  int bo = 1;
+  for (int o = 1; o <= norders; o++) {
+    double e = err[o - 1], bps;
+    if (e > 0.0) {
+      bps = 0.5 * ora_det_log2(0.5 * e / (double)n);
+      if (bps < 0.0) bps = 0.0;
+    } else if (e < 0.0) bps = 1e32;
+    else bps = 0.0;
+    double bits = bps * (double)(n - o) + (double)(o * overhead_per_order);
+    if (o == 1 || bits < best) { best = bits; bo = o; }
+  }
+  return bo;
+}
+
+/* ---------------------------------------------------------------- Rice estimation (3.8) */
+static uint64_t rice_est2(uint64_t n, uint64_t S, int k) {
+  uint64_t lo = n * (uint64_t)((1u << k) - 1u);
+  uint64_t tail = (2 * S > lo) ? ((2 * S - lo) >> (k + 1)) : 0;
+  return n * (uint64_t)(k + 1) + tail;
+}
+static void rice_pick(uint64_t n, uint64_t S, int *k_out, uint64_t *bits_out) {
+  uint64_t mean = n ? S / n : 0;
+  int kc = bitlen_u64(mean);
+  int lo = kc - 2 < 0 ? 0 : kc - 2, hi = kc + 1 > 30 ? 30 : kc + 1;
+  uint64_t best = 0;
+  int bk = lo;
+  for (int k = lo; k <= hi; k++) {
+    uint64_t e = rice_est2(n, S, k);
+    if (k == lo || e < best) { best = e; bk = k; }
+  }
+  *k_out = bk;
+  *bits_out = best;
+}
+
+/* max partition order for block n, predictor order o, level cap */
+static int max_porder(int n, int o, int cap) {
+  int p = 0;
+  while (p < cap && ((n >> (p + 1)) << (p + 1)) == n && (n >> (p + 1)) > o) p++;
+  return p;
+}
+
+/* ================================================================== subframe descriptor */
+typedef struct {
+  int type;  /* 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC */
+  int order;
+  int wasted;
+  int sbps;  /* sample bits written (after wasted-bit shift) */
+  int precision, shift;
+  int32_t coef[32];
+  int porder, method;
+  int k[256];
+  uint64_t bits;  /* exact subframe bits */
+  int32_t cval;   /* constant value */
+} sf_t;
+
+/* residual for model (fixed order o, or LPC with q/shift); returns 0 if |r| exceeds int32 */
+static int compute_residual(const int64_t *s, int n, int type, int o, const int32_t *q, int shift, int64_t *r) {
+  for (int i = o; i < n; i++) {
+    int64_t v;
+    if (type == 2) {
+      switch (o) {
+      case 0: v = s[i]; break;
+      case 1: v = s[i] - s[i - 1]; break;
+      case 2: v = s[i] - 2 * s[i - 1] + s[i - 2]; break;
+      case 3: v = s[i] - 3 * s[i - 1] + 3 * s[i - 2] - s[i - 3]; break;
+      default: v = s[i] - 4 * s[i - 1] + 6 * s[i - 2] - 4 * s[i - 3] + s[i - 4]; break;
+      }
+    } else {
+      int64_t sum = 0;
+      for (int j = 0; j < o; j++) sum += (int64_t)q[j] * s[i - 1 - j];
+      v = s[i] - (sum >> shift);
+    }
+    if (v > INT32_MAX || v < INT32_MIN) return 0;
+    r[i] = v;
+  }
+  return 1;
+}
+static inline uint64_t zz(int64_t r) { return r >= 0 ? (uint64_t)r << 1 : ((uint64_t)(-(r + 1)) << 1) | 1u; }
+
+/* Estimated residual bits for a model + best partition order (3.8). Fills porder & k[]. */
+static uint64_t residual_estimate(const int64_t *r, int n, int o, int pcap, int *porder_out, int *k_out) {
+  int pmax = max_porder(n, o, pcap);
+  uint64_t sums[256];
+  int np = 1 << pmax, ps = n >> pmax;
+  for (int j = 0; j < np; j++) {
+    uint64_t S = 0;
+    int a = j == 0 ? o : j * ps, b = (j + 1) * ps;
+    for (int i = a; i < b; i++) S += zz(r[i]);
+    sums[j] = S;
+  }
+  uint64_t best = 0;
+  int bp = 0;
+  int kbest[256];
+  for (int p = pmax; p >= 0; p--) {
+    int npp = 1 << p, psz = n >> p;
+    uint64_t tot = 0;
+    int anybig = 0;
+    int kk[256];
+    for (int j = 0; j < npp; j++) {
+      uint64_t cnt = (uint64_t)(psz - (j == 0 ? o : 0));
+      uint64_t bits;
+      rice_pick(cnt, sums[j], &kk[j], &bits);
+      if (kk[j] > 14) anybig = 1;
+      tot += bits;
+    }
+    tot += (uint64_t)npp * (anybig ? 5 : 4) + 6;
+    if (p == pmax || tot <= best) { /* iterate high->low, '<=' : ties -> smaller p */
+      best = tot;
+      bp = p;
+      memcpy(kbest, kk, sizeof(int) * npp);
+    }
+    /* merge sums to the next coarser order */
+    for (int j = 0; j < npp / 2; j++) sums[j] = sums[2 * j] + sums[2 * j + 1];
+  }
+  *porder_out = bp;
+  memcpy(k_out, kbest, sizeof(int) * (1 << bp));
+  return best;
+}
+
+/* exact refinement of k per partition (+-1), returns exact residual bits */
+static uint64_t residual_exact(const int64_t *r, int n, int o, int porder, int *k, int *method_out) {
+  int np = 1 << porder, ps = n >> porder;
+  uint64_t tot = 6;
+  int anybig = 0;
+  for (int j = 0; j < np; j++) {
+    int a = j == 0 ? o : j * ps, b = (j + 1) * ps;
+    uint64_t cnt = (uint64_t)(b - a);
+    int k0 = k[j];
+    uint64_t best = 0;
+    int bk = k0;
+    int first = 1;
+    for (int kk = k0 - 1; kk <= k0 + 1; kk++) {
+      if (kk < 0 || kk > 30) continue;
+      uint64_t e = cnt * (uint64_t)(kk + 1);
+      for (int i = a; i < b; i++) e += zz(r[i]) >> kk;
+      if (first || e < best) { best = e; bk = kk; first = 0; }
+    }
+    k[j] = bk;
+    if (bk > 14) anybig = 1;
+    tot += best;
+  }
+  tot += (uint64_t)np * (anybig ? 5 : 4);
+  *method_out = anybig;
+  return tot;
+}
+
+typedef struct {
+  int nwin;
+  int n;
+  const float *win; /* nwin * n */
+} winset_t;
+
+/* Encode decision for one subframe. s = channel samples (int64), n = block. */
+static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cfg *cfg, const winset_t *ws,
+                             sf_t *d, int64_t *s, int64_t *r, int64_t *rbest, float *wf) {
+  memset(d, 0, sizeof(*d));
+  /* 3.2 constant */
+  int allsame = 1;
+  uint64_t orv = 0;
+  for (int i = 0; i < n; i++) {
+    if (s_in[i] != s_in[0]) allsame = 0;
+    orv |= (uint64_t)s_in[i];
+  }
+  if (allsame) {
+    d->type = 0;
+    d->sbps = bps;
+    d->cval = (int32_t)s_in[0];
+    d->bits = 8 + (uint64_t)bps;
+    return;
+  }
+  /* 3.3 wasted bits */
+  int w = 0;
+  while (!((orv >> w) & 1)) w++;
+  int sbps = bps - w;
+  for (int i = 0; i < n; i++) s[i] = s_in[i] >> w;
+  uint64_t hdr = 8 + (uint64_t)(w ? w : 0);
+  uint64_t verb = hdr + (uint64_t)n * (uint64_t)sbps;
+
+  int btype = -1, border = 0, bporder = 0, bshift = 0, bprec = 0;
+  int32_t bcoef[32];
+  int bk[256];
+  uint64_t best_est = 0;
+
+  /* candidate list: FIXED 0..4 then LPC orders of window 0 then one LPC per extra window */
+  int fmax = n - 1 < 4 ? n - 1 : 4;
+  for (int o = 0; o <= fmax; o++) {
+    compute_residual(s, n, 2, o, NULL, 0, r);
+    int po, kk[256];
+    uint64_t e = hdr + (uint64_t)o * sbps + residual_estimate(r, n, o, cfg->max_porder, &po, kk);
+    if (btype < 0 || e < best_est) {
+      best_est = e; btype = 2; border = o; bporder = po;
+      memcpy(bk, kk, sizeof(int) * (1 << po));
+      memcpy(rbest, r, sizeof(int64_t) * n);
+    }
+  }
+  int lmax = cfg->max_lpc < n - 1 ? cfg->max_lpc : n - 1;
+  if (cfg->nsub > 0 && lmax > 0) {
+    int prec = qlp_precision(bps, n);
+    for (int wi = 0; wi < ws->nwin; wi++) {
+      const float *win = ws->win + (size_t)wi * n;
+      for (int i = 0; i < n; i++) wf[i] = (float)s[i] * win[i];
+      double autoc[33];
+      ora_autocorr(wf, n, lmax, autoc);
+      if (!(autoc[0] != 0.0)) continue;
+      double lp[32 * 32], err[32];
+      int nord = ora_levinson(autoc, lmax, lp, err);
+      int olo = 1, ohi = nord;
+      if (wi > 0) { olo = ohi = best_order_by_error(err, nord, n, prec + sbps); }
+      for (int o = olo; o <= ohi; o++) {
+        int32_t q[32];
+        int sh;
+        if (ora_quantize(lp + (o - 1) * 32, o, prec, q, &sh) != 0) continue;
+        if (!compute_residual(s, n, 3, o, q, sh, r)) continue;
+        int po, kk[256];
+        uint64_t e = hdr + (uint64_t)o * sbps + 4 + 5 + (uint64_t)o * prec +
+                     residual_estimate(r, n, o, cfg->max_porder, &po, kk);
+        if (e < best_est) {
+          best_est = e; btype = 3; border = o; bporder = po; bshift = sh; bprec = prec;
+          memcpy(bcoef, q, sizeof(int32_t) * o);
+          memcpy(bk, kk, sizeof(int) * (1 << po));
+          memcpy(rbest, r, sizeof(int64_t) * n);
+        }
+      }
+    }
+  }
+  /* 3.9 exact bits for the winner, compare with verbatim */
+  int method;
+  uint64_t exact = hdr + (uint64_t)border * sbps + (btype == 3 ? 4 + 5 + (uint64_t)border * bprec : 0) +
+                   residual_exact(rbest, n, border, bporder, bk, &method);
+  d->wasted = w;
+  d->sbps = sbps;
+  if (exact >= verb) {
+    d->type = 1;
+    d->bits = verb;
+    return;
+  }
+  d->type = btype;
+  d->order = border;
+  d->porder = bporder;
+  d->method = method;
+  d->shift = bshift;
+  d->precision = bprec;
+  memcpy(d->k, bk, sizeof(int) * (1 << bporder));
+  if (btype == 3) memcpy(d->coef, bcoef, sizeof(int32_t) * border);
+  d->bits = exact;
+}
+
+/* write one subframe (samples s = shifted samples when wasted > 0) */
+static void write_subframe(bw_t *bw, const sf_t *d, const int64_t *s, const int64_t *r, int n) {
+  uint64_t start = bw->bits;
+  bw_put(bw, 0, 1);
+  int tcode = d->type == 0 ? 0 : d->type == 1 ? 1 : d->type == 2 ? 8 + d->order : 31 + d->order;
+  bw_put(bw, (uint64_t)tcode, 6);
+  if (d->type != 0 && d->wasted) {
+    bw_put(bw, 1, 1);
+    bw_zeros(bw, (uint64_t)(d->wasted - 1));
+    bw_put(bw, 1, 1);
+  } else bw_put(bw, 0, 1);
+  uint64_t msk = d->sbps >= 64 ? ~0ull : ((1ull << d->sbps) - 1);
+  if (d->type == 0) {
+    bw_put(bw, (uint64_t)(int64_t)d->cval & msk, d->sbps);
+  } else if (d->type == 1) {
+    for (int i = 0; i < n; i++) bw_put(bw, (uint64_t)s[i] & msk, d->sbps);
+  } else {
+    for (int i = 0; i < d->order; i++) bw_put(bw, (uint64_t)s[i] & msk, d->sbps);
+    if (d->type == 3) {
+      bw_put(bw, (uint64_t)(d->precision - 1), 4);
+      bw_put(bw, (uint64_t)d->shift & 31, 5);
+      for (int j = 0; j < d->order; j++) bw_put(bw, (uint64_t)(int64_t)d->coef[j] & ((1ull << d->precision) - 1), d->precision);
+    }
+    bw_put(bw, (uint64_t)d->method, 2);
+    bw_put(bw, (uint64_t)d->porder, 4);
+    int np = 1 << d->porder, ps = n >> d->porder;
+    int pb = d->method ? 5 : 4;
+    for (int j = 0; j < np; j++) {
+      int k = d->k[j];
+      bw_put(bw, (uint64_t)k, pb);
+      int a = j == 0 ? d->order : j * ps, b = (j + 1) * ps;
+      for (int i = a; i < b; i++) {
+        uint64_t u = zz(r[i]);
+        bw_zeros(bw, u >> k);
+        bw_put(bw, 1, 1);
+        if (k) bw_put(bw, u & ((1ull << k) - 1), k);
+      }
+    }
+  }
+  (void)start;
+}
+
+/* ---------------------------------------------------------------- frame header (RFC 9639 9.1) */
+static int bs_code(int bs, int *extra_bits) {
+  *extra_bits = 0;
+  if (bs == 192) return 1;
+  if (bs == 576) return 2;
+  if (bs == 1152) return 3;
+  if (bs == 2304) return 4;
+  if (bs == 4608) return 5;
+  for (int c = 8; c <= 15; c++)
+    if (bs == (256 << (c - 8))) return c;
+  if (bs <= 256) { *extra_bits = 8; return 6; }
+  *extra_bits = 16;
+  return 7;
+}
+static int sr_code(int sr, int *extra_bits, int *extra_val) {
+  *extra_bits = 0;
+  *extra_val = 0;
+  switch (sr) {
+  case 88200: return 1;
+  case 176400: return 2;
+  case 192000: return 3;
+  case 8000: return 4;
+  case 16000: return 5;
+  case 22050: return 6;
+  case 24000: return 7;
+  case 32000: return 8;
+  case 44100: return 9;
+  case 48000: return 10;
+  case 96000: return 11;
+  }
+  if (sr % 1000 == 0 && sr / 1000 <= 255) { *extra_bits = 8; *extra_val = sr / 1000; return 12; }
+  if (sr <= 65535) { *extra_bits = 16; *extra_val = sr; return 13; }
+  if (sr % 10 == 0 && sr / 10 <= 65535) { *extra_bits = 16; *extra_val = sr / 10; return 14; }
+  return 0;
+}
+static int bps_code(int bps) {
+  switch (bps) {
+  case 8: return 1;
+  case 12: return 2;
+  case 16: return 4;
+  case 20: return 5;
+  case 24: return 6;
+  case 32: return 7;
+  }
+  return 0;
+}
+static void put_utf8(bw_t *bw, uint64_t v) {
+  if (v < 0x80) { bw_put(bw, v, 8); return; }
+  int nb;
+  if (v < 0x800) nb = 2;
+  else if (v < 0x10000) nb = 3;
+  else if (v < 0x200000) nb = 4;
+  else if (v < 0x4000000) nb = 5;
+  else if (v < 0x80000000ull) nb = 6;
+  else nb = 7;
+  int first_bits = 7 - nb; /* payload bits in first byte */
+  uint64_t lead = (0xFF00u >> nb) & 0xFF;
+  bw_put(bw, lead | (v >> (6 * (nb - 1))), 8);
+  (void)first_bits;
+  for (int i = nb - 2; i >= 0; i--) bw_put(bw, 0x80 | ((v >> (6 * i)) & 0x3F), 8);
+}
+
+/* ---------------------------------------------------------------- stream header (F4) */
+static const char VENDOR[] = "flac-raster-amd 0.1.0 gfx950 HIP"; /* 32 bytes, same length as libFLAC's */
+
+ORA_API size_t ora_stream_header(uint8_t *out /* >= 86 */, int channels, int bps, int sample_rate, int blocksize) {
+  bw_t bw = {0};
+  bw_put(&bw, 0x664C6143u, 32); /* fLaC */
+  bw_put(&bw, 0, 1);            /* not last */
+  bw_put(&bw, 0, 7);            /* STREAMINFO */
+  bw_put(&bw, 34, 24);
+  bw_put(&bw, (uint64_t)blocksize, 16);
+  bw_put(&bw, (uint64_t)blocksize, 16);
+  bw_put(&bw, 0, 24);
+  bw_put(&bw, 0, 24);
+  bw_put(&bw, (uint64_t)sample_rate, 20);
+  bw_put(&bw, (uint64_t)(channels - 1), 3);
+  bw_put(&bw, (uint64_t)(bps - 1), 5);
+  bw_put(&bw, 0, 36);
+  bw_zeros(&bw, 128);
+  bw_put(&bw, 1, 1);  /* last */
+  bw_put(&bw, 4, 7);  /* VORBIS_COMMENT */
+  size_t vlen = sizeof(VENDOR) - 1;
+  bw_put(&bw, 4 + vlen + 4, 24);
+  size_t pos = (size_t)(bw.bits / 8);
+  bw_reserve(&bw, (4 + vlen + 4) * 8);
+  uint8_t *p = bw.buf + pos;
+  p[0] = (uint8_t)vlen; p[1] = (uint8_t)(vlen >> 8); p[2] = (uint8_t)(vlen >> 16); p[3] = (uint8_t)(vlen >> 24);
+  memcpy(p + 4, VENDOR, vlen);
+  memset(p + 4 + vlen, 0, 4);
+  size_t total = pos + 4 + vlen + 4;
+  memcpy(out, bw.buf, total);
+  free(bw.buf);
+  return total;
+}
+
+/* ================================================================== encoder entry points */
+typedef struct {
+  int64_t frames;
+  int64_t type_count[4];
+} ora_stats;
+
+static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps, int sr, int blocksize,
+                          int level, int64_t *frame_bytes /* optional */, int32_t *sf_info /* optional, 4 per sf */) {
+  const level_cfg *cfg = &LEVELS[level < 0 ? 0 : level > 8 ? 8 : level];
+  int64_t nframes = (N + blocksize - 1) / blocksize;
+  int64_t *s_in = (int64_t *)malloc(sizeof(int64_t) * blocksize);
+  int64_t *r = (int64_t *)malloc(sizeof(int64_t) * blocksize);
+  int64_t *rb = (int64_t *)malloc(sizeof(int64_t) * C * blocksize);
+  int64_t *sh = (int64_t *)malloc(sizeof(int64_t) * C * blocksize);
+  float *wf = (float *)malloc(sizeof(float) * blocksize);
+  int nwin = ora_num_windows(cfg->nsub);
+  float *winfull = nwin ? (float *)malloc(sizeof(float) * nwin * blocksize) : NULL;
+  float *winpart = nwin ? (float *)malloc(sizeof(float) * nwin * blocksize) : NULL;
+  if (nwin) ora_window_set(winfull, blocksize, cfg->nsub);
+  sf_t *d = (sf_t *)malloc(sizeof(sf_t) * C);
+  for (int64_t f = 0; f < nframes; f++) {
+    int n = (int)((N - f * blocksize) < blocksize ? (N - f * blocksize) : blocksize);
+    winset_t ws = {nwin, n, winfull};
+    if (nwin && n != blocksize) { ora_window_set(winpart, n, cfg->nsub); ws.win = winpart; }
+    for (int c = 0; c < C; c++) {
+      for (int i = 0; i < n; i++) s_in[i] = x[(f * blocksize + i) * C + c];
+      analyze_subframe(s_in, n, bps, cfg, &ws, &d[c], sh + (size_t)c * blocksize, r, rb + (size_t)c * blocksize, wf);
+      if (d[c].type == 0) { /* constant: analysis returned before filling the shifted copy */
+        for (int i = 0; i < n; i++) sh[(size_t)c * blocksize + i] = s_in[i];
+      }
+      if (sf_info) {
+        int32_t *o = sf_info + ((f * C + c) * 4);
+        o[0] = d[c].type; o[1] = d[c].order; o[2] = d[c].porder; o[3] = (int32_t)d[c].bits;
+      }
+    }
+    /* frame header */
+    uint64_t fstart = bw->bits;
+    int bsx, srx, srv;
+    int bcode = bs_code(n, &bsx);
+    int scode = sr_code(sr, &srx, &srv);
+    bw_put(bw, 0xFFF8, 16);
+    bw_put(bw, (uint64_t)bcode, 4);
+    bw_put(bw, (uint64_t)scode, 4);
+    bw_put(bw, (uint64_t)(C - 1), 4);
+    bw_put(bw, (uint64_t)bps_code(bps), 3);
+    bw_put(bw, 0, 1);
+    put_utf8(bw, (uint64_t)f);
+    if (bsx) bw_put(bw, (uint64_t)(n - 1), bsx);
+    if (srx) bw_put(bw, (uint64_t)srv, srx);
+    size_t hb = (size_t)((bw->bits - fstart) / 8);
+    bw_put(bw, ora_crc8(bw->buf + fstart / 8, hb), 8);
+    for (int c = 0; c < C; c++) {
+      write_subframe(bw, &d[c], sh + (size_t)c * blocksize, rb + (size_t)c * blocksize, n);
+    }
+    bw_align(bw);
+    size_t flen = (size_t)((bw->bits - fstart) / 8);
+    bw_put(bw, ora_crc16(bw->buf + fstart / 8, flen), 16);
+    if (frame_bytes) frame_bytes[f] = (int64_t)((bw->bits - fstart) / 8);
+  }
+  free(s_in); free(r); free(rb); free(sh); free(wf); free(winfull); free(winpart); free(d);
+}
+
+/* Encode a whole stream (pyflac StreamEncoder(...).process(x); finish() equivalent).
+ * x: interleaved int32 (N x C).  with_header: prepend fLaC+STREAMINFO+VORBIS_COMMENT (86 B).
+ * Returns malloc'ed buffer in *out (free with ora_free). */
+ORA_API int ora_encode(const int32_t *x, int64_t N, int C, int bps, int sample_rate, int blocksize, int level,
+                       int with_header, uint8_t **out, size_t *outlen, int64_t *frame_bytes, int32_t *sf_info) {
+  if (C < 1 || C > 8 || blocksize < 16 || blocksize > 65535 || (bps != 16 && bps != 32 && (bps < 4 || bps > 32)))
+    return -1;
+  bw_t bw = {0};
+  if (with_header) {
+    uint8_t h[128];
+    size_t hl = ora_stream_header(h, C, bps, sample_rate, blocksize);
+    bw_reserve(&bw, hl * 8);
+    memcpy(bw.buf, h, hl);
+    bw.bits = hl * 8;
+  }
+  encode_frames(&bw, x, N, C, bps, sample_rate, blocksize, level, frame_bytes, sf_info);
+  *out = bw.buf;
+  *outlen = (size_t)(bw.bits / 8);
+  return 0;
+}
+ORA_API void ora_free(void *p) { free(p); }
+
+/* ================================================================== decoder */
+typedef struct {
+  const uint8_t *p;
+  size_t len;
+  uint64_t pos; /* bit position */
+  int err;
+} br_t;
+static uint64_t br_get(br_t *b, int nb) {
+  uint64_t v = 0;
+  for (int i = 0; i < nb; i++) {
+    if ((b->pos >> 3) >= b->len) { b->err = 1; return 0; }
+    v = (v << 1) | ((b->p[b->pos >> 3] >> (7 - (b->pos & 7))) & 1);
+    b->pos++;
+  }
+  return v;
+}
+static int64_t br_sget(br_t *b, int nb) {
+  if (nb == 0) return 0;
+  uint64_t v = br_get(b, nb);
+  if (nb < 64 && (v >> (nb - 1)) & 1) v |= ~0ull << nb;
+  return (int64_t)v;
+}
+static uint64_t br_unary(br_t *b) {
+  uint64_t q = 0;
+  for (;;) {
+    if ((b->pos >> 3) >= b->len) { b->err = 1; return 0; }
+    if ((b->p[b->pos >> 3] >> (7 - (b->pos & 7))) & 1) { b->pos++; return q; }
+    b->pos++;
+    q++;
+  }
+}
+
+static int decode_subframe(br_t *b, int n, int sbps, int64_t *out) {
+  if (br_get(b, 1) != 0) return -10;
+  int t = (int)br_get(b, 6);
+  int w = 0;
+  if (br_get(b, 1)) w = (int)br_unary(b) + 1;
+  int bps = sbps - w;
+  if (bps <= 0) return -11;
+  if (t == 0) {
+    int64_t v = br_sget(b, bps);
+    for (int i = 0; i < n; i++) out[i] = v;
+  } else if (t == 1) {
+    for (int i = 0; i < n; i++) out[i] = br_sget(b, bps);
+  } else {
+    int order, lpc = 0;
+    if (t >= 8 && t <= 12) order = t - 8;
+    else if (t >= 32) { order = t - 31; lpc = 1; }
+    else return -12;
+    if (order > n) return -13;
+    for (int i = 0; i < order; i++) out[i] = br_sget(b, bps);
+    int64_t q[32];
+    int prec = 0, shift = 0;
+    if (lpc) {
+      prec = (int)br_get(b, 4) + 1;
+      if (prec == 16) return -14;
+      shift = (int)br_sget(b, 5);
+      if (shift < 0) return -15;
+      for (int j = 0; j < order; j++) q[j] = br_sget(b, prec);
+    }
+    int method = (int)br_get(b, 2);
+    if (method > 1) return -16;
+    int porder = (int)br_get(b, 4);
+    int np = 1 << porder;
+    if ((n >> porder) << porder != n && porder > 0) return -17;
+    int ps = n >> porder;
+    if (ps < order) return -18;
+    int pb = method ? 5 : 4, esc = method ? 31 : 15;
+    int64_t *res = out; /* write residuals in place, then reconstruct */
+    for (int j = 0; j < np; j++) {
+      int k = (int)br_get(b, pb);
+      int a = j == 0 ? order : j * ps, e = (j + 1) * ps;
+      if (k == esc) {
+        int rb = (int)br_get(b, 5);
+        for (int i = a; i < e; i++) res[i] = br_sget(b, rb);
+      } else {
+        for (int i = a; i < e; i++) {
+          uint64_t u = (br_unary(b) << k);
+          if (k) u |= br_get(b, k);
+          res[i] = (u & 1) ? -(int64_t)(u >> 1) - 1 : (int64_t)(u >> 1);
+        }
+      }
+      if (b->err) return -19;
+    }
+    for (int i = order; i < n; i++) {
+      int64_t pred;
+      if (!lpc) {
+        switch (order) {
+        case 0: pred = 0; break;
+        case 1: pred = out[i - 1]; break;
+        case 2: pred = 2 * out[i - 1] - out[i - 2]; break;
+        case 3: pred = 3 * out[i - 1] - 3 * out[i - 2] + out[i - 3]; break;
+        default: pred = 4 * out[i - 1] - 6 * out[i - 2] + 4 * out[i - 3] - out[i - 4]; break;
+        }
+      } else {
+        int64_t sum = 0;
+        for (int j = 0; j < order; j++) sum += q[j] * out[i - 1 - j];
+        pred = sum >> shift;
+      }
+      out[i] = res[i] + pred;
+    }
+  }
+  if (w)
+    for (int i = 0; i < n; i++) out[i] = (int64_t)((uint64_t)out[i] << w);
+  return b->err ? -20 : 0;
+}
+
+/* Decode a FLAC stream (fLaC + metadata + frames) or bare frames (skip_header=0/1 auto).
+ * Output interleaved int32 samples (malloc'ed).  Verifies CRC-8/CRC-16.  Returns 0 / <0 error. */
+ORA_API int ora_decode(const uint8_t *buf, size_t len, int32_t **out, int64_t *nsamples, int *channels_out,
+                       int *bps_out, int *sr_out, int64_t *nframes_out) {
+  br_t b = {buf, len, 0, 0};
+  int C = 0, bps = 0, sr = 0;
+  if (len >= 4 && memcmp(buf, "fLaC", 4) == 0) {
+    b.pos = 32;
+    int last = 0;
+    while (!last) {
+      last = (int)br_get(&b, 1);
+      int type = (int)br_get(&b, 7);
+      int blen = (int)br_get(&b, 24);
+      if (b.err) return -1;
+      if (type == 0) {
+        uint64_t p0 = b.pos;
+        br_get(&b, 16); br_get(&b, 16); br_get(&b, 24); br_get(&b, 24);
+        sr = (int)br_get(&b, 20);
+        C = (int)br_get(&b, 3) + 1;
+        bps = (int)br_get(&b, 5) + 1;
+        b.pos = p0 + (uint64_t)blen * 8;
+      } else b.pos += (uint64_t)blen * 8;
+    }
+  }
+  size_t cap = 1 << 16;
+  int32_t *o = (int32_t *)malloc(sizeof(int32_t) * cap);
+  int64_t total = 0, nfr = 0;
+  int64_t *tmp = (int64_t *)malloc(sizeof(int64_t) * 65536 * 2);
+  int64_t *chs[8];
+  for (int c = 0; c < 8; c++) chs[c] = (int64_t *)malloc(sizeof(int64_t) * 65536);
+  int rc = 0;
+  while ((b.pos >> 3) + 2 <= len) {
+    b.pos = (b.pos + 7) & ~7ull;
+    size_t fstart = (size_t)(b.pos >> 3);
+    if (fstart + 2 > len) break;
+    uint64_t sync = br_get(&b, 15);
+    if (sync != 0x7FFC) {
+      if (nfr == 0 && !C) { rc = -2; break; }
+      /* maybe concatenated streams: stop */
+      break;
+    }
+    br_get(&b, 1); /* blocking strategy */
+    int bcode = (int)br_get(&b, 4), scode = (int)br_get(&b, 4), ca = (int)br_get(&b, 4), bcodep = (int)br_get(&b, 3);
+    br_get(&b, 1);
+    /* utf8 number */
+    uint64_t x = br_get(&b, 8);
+    int extra = 0;
+    if (x & 0x80) {
+      while ((x << (extra + 1)) & 0x80) extra++;
+      for (int i = 0; i < extra; i++) br_get(&b, 8);
+    }
+    int n;
+    if (bcode == 1) n = 192;
+    else if (bcode >= 2 && bcode <= 5) n = 576 << (bcode - 2);
+    else if (bcode == 6) n = (int)br_get(&b, 8) + 1;
+    else if (bcode == 7) n = (int)br_get(&b, 16) + 1;
+    else if (bcode >= 8) n = 256 << (bcode - 8);
+    else { rc = -3; break; }
+    if (scode == 12) br_get(&b, 8);
+    else if (scode == 13 || scode == 14) br_get(&b, 16);
+    int fbps;
+    switch (bcodep) {
+    case 0: fbps = bps; break;
+    case 1: fbps = 8; break;
+    case 2: fbps = 12; break;
+    case 4: fbps = 16; break;
+    case 5: fbps = 20; break;
+    case 6: fbps = 24; break;
+    case 7: fbps = 32; break;
+    default: fbps = 0;
+    }
+    if (!fbps) { rc = -4; break; }
+    size_t hlen = (size_t)((b.pos >> 3) - fstart);
+    unsigned crc8 = (unsigned)br_get(&b, 8);
+    if (crc8 != ora_crc8(buf + fstart, hlen)) { rc = -5; break; }
+    int fc = ca < 8 ? ca + 1 : 2;
+    if (!C) C = fc;
+    if (fc != C) { rc = -6; break; }
+    for (int c = 0; c < fc; c++) {
+      int sb = fbps;
+      if ((ca == 8 && c == 1) || (ca == 9 && c == 0) || (ca == 10 && c == 1)) sb++;
+      int e = decode_subframe(&b, n, sb, chs[c]);
+      if (e) { rc = e; break; }
+    }
+    if (rc) break;
+    b.pos = (b.pos + 7) & ~7ull;
+    size_t flen = (size_t)((b.pos >> 3) - fstart);
+    unsigned crc16 = (unsigned)br_get(&b, 16);
+    if (b.err) { rc = -7; break; }
+    if (crc16 != ora_crc16(buf + fstart, flen)) { rc = -8; break; }
+    for (int i = 0; i < n; i++) {
+      if (ca == 8) chs[1][i] = chs[0][i] - chs[1][i];
+      else if (ca == 9) chs[0][i] = chs[1][i] + chs[0][i];
+      else if (ca == 10) {
+        int64_t m = chs[0][i], s = chs[1][i];
+        m = (int64_t)((uint64_t)m << 1) | (s & 1);
+        chs[0][i] = (m + s) >> 1;
+        chs[1][i] = (m - s) >> 1;
+      }
+    }
+    if ((size_t)((total + n) * fc) > cap) {
+      while ((size_t)((total + n) * fc) > cap) cap *= 2;
+      o = (int32_t *)realloc(o, sizeof(int32_t) * cap);
+    }
+    for (int i = 0; i < n; i++)
+      for (int c = 0; c < fc; c++) o[(total + i) * fc + c] = (int32_t)chs[c][i];
+    total += n;
+    nfr++;
+    if (!bps) bps = fbps;
+  }
+  free(tmp);
+  for (int c = 0; c < 8; c++) free(chs[c]);
+  if (rc) { free(o); return rc; }
+  *out = o;
+  *nsamples = total;
+  *channels_out = C;
+  *bps_out = bps;
+  *sr_out = sr;
+  if (nframes_out) *nframes_out = nfr;
+  return 0;
+}
