@@ -1,0 +1,545 @@
+// fra_api.hip -- host orchestration + C ABI (include/flac_raster_amd.h) of the MI355X encoder.
+//
+// A plan owns every device buffer a job needs (raster copy if host-resident, stream/frame tables,
+// window tables, subframe descriptors, frame sizes/offsets, output, scan workspace), so that
+// fra_plan_execute() only enqueues kernels on the context's stream: no allocation, no host sync
+// (graph-capturable).  Per-job launch sequence (fra_kernels.hip):
+//   k_norm_init, k_minmax, k_norm_finalize  (skipped when norm == 0)
+//   k_analyze  [frames x channels]
+//   k_frame_bytes + hipcub exclusive scan
+//   k_pack     [frames]
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/flac_raster_amd.h"
+#include "fra_internal.h"
+
+namespace fra {
+hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, hipStream_t s);
+hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
+hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
+hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
+hipError_t launch_pack(int src, bool b32, const JobArgs& a, hipStream_t s);
+hipError_t launch_synth(int kind, uint64_t seed, int bands, int H, int W, void* out, hipStream_t s);
+}  // namespace fra
+
+using namespace fra;
+
+static thread_local std::string g_err;
+static int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIPCHK(x)                                                                                \
+  do {                                                                                           \
+    hipError_t _e = (x);                                                                         \
+    if (_e != hipSuccess) return set_err(FRA_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(_e), \
+                                         __FILE__, __LINE__);                                    \
+  } while (0)
+
+struct fra_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+struct fra_plan {
+  fra_ctx* ctx = nullptr;
+  fra_job job{};
+  std::vector<fra_window> windows;
+  std::vector<StreamDev> streams;
+  std::vector<FrameDev> frames;
+  int src = 0;
+  bool b32 = false;
+  int nwin = 0;
+  int max_segs = 0;
+  int cmax = 1;
+  size_t raster_bytes = 0;
+  // device buffers
+  void* d_raster_owned = nullptr;
+  const void* d_raster = nullptr;
+  StreamDev* d_streams = nullptr;
+  FrameDev* d_frames = nullptr;
+  NormDev* d_norm = nullptr;
+  float* d_win = nullptr;
+  SfDesc* d_sf = nullptr;
+  unsigned long long* d_fbytes = nullptr;
+  unsigned long long* d_foff = nullptr;
+  uint8_t* d_out = nullptr;
+  size_t out_cap = 0;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  JobArgs args{};
+  // timing
+  bool timing = false;
+  hipEvent_t ev[5] = {};
+  float ms[4] = {0, 0, 0, 0};
+  int nexec = 0;
+  bool pending_times = false;
+  bool executed = false;
+};
+
+// ----------------------------------------------------------------------------- host helpers
+static int elem_size(int dt) {
+  switch (dt) {
+    case FRA_U8: case FRA_I8: return 1;
+    case FRA_U16: case FRA_I16: return 2;
+    case FRA_U32: case FRA_I32: case FRA_F32: return 4;
+    case FRA_F64: return 8;
+  }
+  return 0;
+}
+// normalization.py:108-120 (calculate_audio_params, total_pixels = H*W of the encode unit)
+static int sample_rate_for_pixels(int64_t px) {
+  if (px < 1000000) return 44100;
+  if (px < 10000000) return 48000;
+  if (px < 100000000) return 96000;
+  return 192000;
+}
+// tukey(p) window as defined in DESIGN.md 3.4 (same formula as the oracle, computed on the host)
+static void tukey(float* w, int N, double p) {
+  for (int i = 0; i < N; i++) w[i] = 1.0f;
+  int Np = (int)(p / 2.0 * (double)N) - 1;
+  if (Np > 0) {
+    for (int n = 0; n <= Np; n++) {
+      w[n] = (float)(0.5 - 0.5 * cos(M_PI * (double)n / (double)Np));
+      w[N - Np - 1 + n] = (float)(0.5 - 0.5 * cos(M_PI * (double)(n + Np) / (double)Np));
+    }
+  }
+}
+static void window_set(float* w, int N, int stride, int nsub) {
+  if (nsub <= 0) return;
+  tukey(w, N, 0.5);
+  int idx = 1;
+  for (int m = 2; m <= nsub; m++)
+    for (int j = 0; j < m; j++, idx++) {
+      float* o = w + (size_t)idx * stride;
+      const int a = (int)((int64_t)j * N / m), b = (int)((int64_t)(j + 1) * N / m);
+      for (int i = 0; i < N; i++) o[i] = 0.0f;
+      if (b - a > 0) tukey(o + a, b - a, 0.5);
+    }
+}
+
+static const char kVendor[] = "flac-raster-amd 0.1.0 gfx950 HIP";  // 32 bytes, as libFLAC's vendor string
+
+extern "C" {
+
+const char* fra_last_error(void) { return g_err.c_str(); }
+int fra_abi_version(void) { return FRA_ABI_VERSION; }
+void fra_free(void* p) { free(p); }
+
+int fra_device_count(int* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return FRA_OK;
+}
+
+int fra_ctx_create(int device, fra_ctx** out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(FRA_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return set_err(FRA_E_INVALID, "device %d out of range (%d devices)", device, n);
+  HIPCHK(hipSetDevice(device));
+  fra_ctx* c = new (std::nothrow) fra_ctx();
+  if (!c) return set_err(FRA_E_NOMEM, "out of host memory");
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { delete c; return set_err(FRA_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+  *out = c;
+  return FRA_OK;
+}
+
+void fra_ctx_destroy(fra_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void fra_plan_destroy(fra_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  (void)hipFree(p->d_raster_owned);
+  (void)hipFree(p->d_streams);
+  (void)hipFree(p->d_frames);
+  (void)hipFree(p->d_norm);
+  (void)hipFree(p->d_win);
+  (void)hipFree(p->d_sf);
+  (void)hipFree(p->d_fbytes);
+  (void)hipFree(p->d_foff);
+  (void)hipFree(p->d_out);
+  (void)hipFree(p->d_scan_tmp);
+  for (auto& e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete p;
+}
+
+static int plan_build(fra_plan* p) {
+  const fra_job& j = p->job;
+  p->src = j.dtype;
+  const int nsub = level_cfg(j.level).nsub;
+  p->nwin = num_windows(nsub);
+  int bps;
+  if (j.norm == 16) bps = 16;
+  else if (j.norm == 24) bps = 32;  // int32 audio -> 32-bps FLAC
+  else bps = (j.dtype == FRA_I16 || j.dtype == FRA_U8 || j.dtype == FRA_I8) ? 16 : 32;
+  p->b32 = bps == 32;
+  p->cmax = j.channels;
+  p->streams.clear();
+  p->frames.clear();
+  std::map<int, int> win_index;  // block size -> window table index
+  std::vector<int> win_sizes;
+  int64_t nf_total = 0;
+  int64_t max_extent = 0;
+  size_t out_cap = 0;
+  for (int w = 0; w < j.nwindows; w++) {
+    const fra_window& wd = p->windows[w];
+    StreamDev st{};
+    st.base_off = (int64_t)wd.row_off * j.row_stride + (int64_t)wd.col_off * j.col_stride;
+    st.band_stride = j.band_stride;
+    st.row_stride = j.row_stride;
+    st.col_stride = j.col_stride;
+    st.width = wd.width;
+    st.height = wd.height;
+    st.channels = j.channels;
+    st.bps = bps;
+    st.norm = j.norm;
+    st.nsamples = (int64_t)wd.width * wd.height;
+    st.sample_rate = j.sample_rate > 0 ? j.sample_rate : sample_rate_for_pixels(st.nsamples);
+    st.first_frame = (int32_t)nf_total;
+    const int64_t nfr = (st.nsamples + j.blocksize - 1) / j.blocksize;
+    st.nframes = (int32_t)nfr;
+    if (st.nsamples > 0) {
+      int64_t ext = st.base_off + (int64_t)(j.channels - 1) * j.band_stride + (int64_t)(wd.height - 1) * j.row_stride +
+                    (int64_t)(wd.width - 1) * j.col_stride + 1;
+      max_extent = std::max(max_extent, ext);
+      const int segs = (wd.width + 4095) / 4096;
+      p->max_segs = (int)std::max<int64_t>(p->max_segs, (int64_t)segs * wd.height);
+    }
+    for (int64_t f = 0; f < nfr; f++) {
+      FrameDev fr{};
+      fr.stream = w;
+      fr.index = (int32_t)f;
+      const int64_t first = f * j.blocksize;
+      fr.n = (int32_t)std::min<int64_t>(j.blocksize, st.nsamples - first);
+      fr.row0 = (int32_t)(first / wd.width);
+      fr.col0 = (int32_t)(first % wd.width);
+      auto it = win_index.find(fr.n);
+      if (it == win_index.end()) {
+        int idx = (int)win_sizes.size();
+        win_index[fr.n] = idx;
+        win_sizes.push_back(fr.n);
+        fr.win = idx;
+      } else fr.win = it->second;
+      p->frames.push_back(fr);
+      out_cap += 16 + 2 + (size_t)j.channels * ((size_t)fr.n * bps / 8 + 8);
+    }
+    nf_total += nfr;
+    p->streams.push_back(st);
+  }
+  if (nf_total > INT32_MAX / 2) return set_err(FRA_E_INVALID, "too many frames (%lld)", (long long)nf_total);
+  p->raster_bytes = (size_t)max_extent * elem_size(j.dtype);
+  p->out_cap = out_cap + 64;
+  const int nfr = (int)nf_total;
+  (void)hipSetDevice(p->ctx->device);
+  HIPCHK(hipMalloc(&p->d_streams, sizeof(StreamDev) * std::max<size_t>(1, p->streams.size())));
+  HIPCHK(hipMalloc(&p->d_frames, sizeof(FrameDev) * std::max(1, nfr)));
+  HIPCHK(hipMalloc(&p->d_norm, sizeof(NormDev) * std::max<size_t>(1, p->streams.size())));
+  HIPCHK(hipMalloc(&p->d_sf, sizeof(SfDesc) * (size_t)std::max(1, nfr) * p->cmax));
+  HIPCHK(hipMalloc(&p->d_fbytes, sizeof(unsigned long long) * (nfr + 1)));
+  HIPCHK(hipMalloc(&p->d_foff, sizeof(unsigned long long) * (nfr + 1)));
+  HIPCHK(hipMalloc(&p->d_out, p->out_cap));
+  const size_t wn = (size_t)std::max<size_t>(1, win_sizes.size()) * std::max(1, p->nwin) * j.blocksize;
+  std::vector<float> wt(wn, 0.0f);
+  for (size_t t = 0; t < win_sizes.size(); t++)
+    window_set(wt.data() + t * std::max(1, p->nwin) * j.blocksize, win_sizes[t], j.blocksize, nsub);
+  HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wn));
+  HIPCHK(hipMemcpy(p->d_win, wt.data(), sizeof(float) * wn, hipMemcpyHostToDevice));
+  if (!p->streams.empty())
+    HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
+  if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(p->d_norm, 0, sizeof(NormDev) * std::max<size_t>(1, p->streams.size())));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, p->scan_tmp_bytes, p->d_fbytes, p->d_foff, nfr + 1,
+                                          p->ctx->stream));
+  HIPCHK(hipMalloc(&p->d_scan_tmp, std::max<size_t>(16, p->scan_tmp_bytes)));
+  JobArgs& a = p->args;
+  a.streams = p->d_streams;
+  a.frames = p->d_frames;
+  a.norm = p->d_norm;
+  a.win = p->d_win;
+  a.sf = p->d_sf;
+  a.frame_bytes = p->d_fbytes;
+  a.frame_off = p->d_foff;
+  a.out = p->d_out;
+  a.nframes_total = nfr;
+  a.cmax = p->cmax;
+  a.blocksize = j.blocksize;
+  a.level = j.level;
+  a.nwin = std::max(1, p->nwin);
+  for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
+  return FRA_OK;
+}
+
+int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  (void)hipSetDevice(p->ctx->device);
+  if (on_device) {
+    p->d_raster = raster;
+  } else {
+    if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
+    if (p->raster_bytes)
+      HIPCHK(hipMemcpyAsync(p->d_raster_owned, raster, p->raster_bytes, hipMemcpyHostToDevice, p->ctx->stream));
+    p->d_raster = p->d_raster_owned;
+  }
+  p->args.raster = p->d_raster;
+  p->job.raster = raster;
+  p->job.raster_on_device = on_device;
+  return FRA_OK;
+}
+
+int fra_plan_create(fra_ctx* ctx, const fra_job* job, fra_plan** out) {
+  if (!ctx || !job || !out) return set_err(FRA_E_INVALID, "null argument");
+  if (job->channels < 1 || job->channels > 8) return set_err(FRA_E_INVALID, "channels must be 1..8 (got %d)", job->channels);
+  if (job->blocksize < 16 || job->blocksize > kMaxBlock)
+    return set_err(FRA_E_INVALID, "blocksize must be 16..%d (got %d)", kMaxBlock, job->blocksize);
+  if (job->level < 0 || job->level > 8) return set_err(FRA_E_INVALID, "level must be 0..8 (got %d)", job->level);
+  if (job->dtype < FRA_U8 || job->dtype > FRA_F64) return set_err(FRA_E_INVALID, "bad dtype %d", job->dtype);
+  if (job->norm != 0 && job->norm != 16 && job->norm != 24) return set_err(FRA_E_INVALID, "norm must be 0, 16 or 24");
+  if (job->norm == 0 && job->dtype != FRA_I16 && job->dtype != FRA_I32)
+    return set_err(FRA_E_INVALID, "norm == 0 (pre-normalised audio) needs int16 or int32 samples");
+  if (job->nwindows < 0 || (job->nwindows > 0 && !job->windows)) return set_err(FRA_E_INVALID, "bad windows");
+  for (int w = 0; w < job->nwindows; w++) {
+    const fra_window& wd = job->windows[w];
+    if (wd.height < 0 || wd.width < 0 || wd.row_off < 0 || wd.col_off < 0 || (wd.height > 0) != (wd.width > 0))
+      return set_err(FRA_E_INVALID, "window %d invalid (%d,%d,%d,%d)", w, wd.row_off, wd.col_off, wd.height, wd.width);
+  }
+  fra_plan* p = new (std::nothrow) fra_plan();
+  if (!p) return set_err(FRA_E_NOMEM, "out of host memory");
+  p->ctx = ctx;
+  p->job = *job;
+  p->windows.assign(job->windows, job->windows + job->nwindows);
+  p->job.windows = p->windows.data();
+  int rc = plan_build(p);
+  if (rc == FRA_OK && job->raster) rc = fra_plan_set_raster(p, job->raster, job->raster_on_device);
+  if (rc != FRA_OK) {
+    std::string keep = g_err;
+    fra_plan_destroy(p);
+    g_err = keep;
+    return rc;
+  }
+  *out = p;
+  return FRA_OK;
+}
+
+static void collect_times(fra_plan* p) {
+  if (!p->pending_times) return;
+  hipEventSynchronize(p->ev[4]);
+  for (int k = 0; k < 4; k++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p->ev[k], p->ev[k + 1]) == hipSuccess) p->ms[k] += ms;
+  }
+  p->nexec++;
+  p->pending_times = false;
+}
+
+int fra_plan_execute(fra_plan* p) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  if (!p->d_raster && !p->streams.empty()) return set_err(FRA_E_STATE, "plan has no raster");
+  (void)hipSetDevice(p->ctx->device);
+  hipStream_t s = p->ctx->stream;
+  if (p->timing) collect_times(p);
+  const JobArgs& a = p->args;
+  const int nstreams = (int)p->streams.size();
+  if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));
+  if (p->job.norm != 0 && nstreams > 0 && p->max_segs > 0) {
+    HIPCHK(launch_minmax(p->src, a, nstreams, p->max_segs, s));
+    HIPCHK(launch_norm_finalize(a, nstreams, s));
+  }
+  if (p->timing) HIPCHK(hipEventRecord(p->ev[1], s));
+  if (a.nframes_total > 0) HIPCHK(launch_analyze(p->src, p->b32, a, s));
+  if (p->timing) HIPCHK(hipEventRecord(p->ev[2], s));
+  HIPCHK(launch_frame_bytes(a, s));
+  size_t tb = p->scan_tmp_bytes;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(p->d_scan_tmp, tb, p->d_fbytes, p->d_foff, a.nframes_total + 1, s));
+  if (p->timing) HIPCHK(hipEventRecord(p->ev[3], s));
+  if (a.nframes_total > 0) HIPCHK(launch_pack(p->src, p->b32, a, s));
+  if (p->timing) {
+    HIPCHK(hipEventRecord(p->ev[4], s));
+    p->pending_times = true;
+  }
+  p->executed = true;
+  return FRA_OK;
+}
+
+int fra_plan_sync(fra_plan* p) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  (void)hipSetDevice(p->ctx->device);
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  if (p->timing) collect_times(p);
+  return FRA_OK;
+}
+
+int fra_plan_result(fra_plan* p, fra_stream_info* infos, uint64_t* total) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  if (!p->executed) return set_err(FRA_E_STATE, "plan not executed");
+  (void)hipSetDevice(p->ctx->device);
+  const int nfr = p->args.nframes_total;
+  std::vector<unsigned long long> off(nfr + 1);
+  HIPCHK(hipMemcpy(off.data(), p->d_foff, sizeof(unsigned long long) * (nfr + 1), hipMemcpyDeviceToHost));
+  // exclusive scan of [bytes..., 0]: off[nfr] = total
+  if (total) *total = off[nfr];
+  if (infos) {
+    std::vector<NormDev> nd(p->streams.size());
+    if (!nd.empty())
+      HIPCHK(hipMemcpy(nd.data(), p->d_norm, sizeof(NormDev) * nd.size(), hipMemcpyDeviceToHost));
+    for (size_t s = 0; s < p->streams.size(); s++) {
+      const StreamDev& st = p->streams[s];
+      fra_stream_info& in = infos[s];
+      in.offset = off[st.first_frame];
+      in.frame_bytes = off[st.first_frame + st.nframes] - off[st.first_frame];
+      in.data_min = p->job.norm ? nd[s].mn : 0.0;
+      in.data_max = p->job.norm ? nd[s].mx : 0.0;
+      in.sample_rate = st.sample_rate;
+      in.bps = st.bps;
+      in.channels = st.channels;
+      in.nframes = st.nframes;
+    }
+  }
+  return FRA_OK;
+}
+
+int fra_plan_download(fra_plan* p, uint8_t* host_out, uint64_t capacity) {
+  uint64_t total = 0;
+  int rc = fra_plan_result(p, nullptr, &total);
+  if (rc) return rc;
+  if (capacity < total) return set_err(FRA_E_INVALID, "capacity %llu < %llu", (unsigned long long)capacity,
+                                       (unsigned long long)total);
+  if (total) HIPCHK(hipMemcpy(host_out, p->d_out, total, hipMemcpyDeviceToHost));
+  return FRA_OK;
+}
+
+int fra_plan_device_output(fra_plan* p, const uint8_t** dev_ptr, uint64_t* capacity) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  *dev_ptr = p->d_out;
+  *capacity = p->out_cap;
+  return FRA_OK;
+}
+
+int fra_plan_enable_timing(fra_plan* p, int32_t on) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  p->timing = on != 0;
+  for (float& m : p->ms) m = 0;
+  p->nexec = 0;
+  p->pending_times = false;
+  return FRA_OK;
+}
+
+int fra_plan_timing(fra_plan* p, float* ms4, int32_t* n) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  collect_times(p);
+  for (int k = 0; k < 4; k++) ms4[k] = p->ms[k];
+  *n = p->nexec;
+  return FRA_OK;
+}
+
+int fra_encode(int device, const fra_job* job, uint8_t** out, uint64_t* out_len, fra_stream_info* infos) {
+  fra_ctx* ctx = nullptr;
+  int rc = fra_ctx_create(device, &ctx);
+  if (rc) return rc;
+  fra_plan* p = nullptr;
+  rc = fra_plan_create(ctx, job, &p);
+  if (!rc) rc = fra_plan_execute(p);
+  if (!rc) rc = fra_plan_sync(p);
+  uint64_t total = 0;
+  if (!rc) rc = fra_plan_result(p, infos, &total);
+  if (!rc) {
+    *out = (uint8_t*)malloc(total ? total : 1);
+    if (!*out) rc = set_err(FRA_E_NOMEM, "malloc %llu", (unsigned long long)total);
+    else rc = fra_plan_download(p, *out, total);
+    if (rc) { free(*out); *out = nullptr; }
+    *out_len = total;
+  }
+  std::string keep = g_err;
+  fra_plan_destroy(p);
+  fra_ctx_destroy(ctx);
+  g_err = keep;
+  return rc;
+}
+
+int fra_stream_header(uint8_t* o, int32_t channels, int32_t bps, int32_t sample_rate, int32_t blocksize) {
+  if (!o || channels < 1 || channels > 8 || bps < 4 || bps > 32 || blocksize < 16 || blocksize > 65535 ||
+      sample_rate <= 0 || sample_rate >= (1 << 20))
+    return set_err(FRA_E_INVALID, "bad stream header parameters");
+  memcpy(o, "fLaC", 4);
+  o[4] = 0x00;  // STREAMINFO, not last
+  o[5] = 0; o[6] = 0; o[7] = 34;
+  uint8_t* si = o + 8;
+  memset(si, 0, 34);
+  si[0] = (uint8_t)(blocksize >> 8); si[1] = (uint8_t)blocksize;
+  si[2] = (uint8_t)(blocksize >> 8); si[3] = (uint8_t)blocksize;
+  // bytes 4..9 min/max frame size = 0
+  // 20-bit sample rate | 3-bit channels-1 | 5-bit bps-1 | 36-bit total samples (0)
+  si[10] = (uint8_t)(sample_rate >> 12);
+  si[11] = (uint8_t)(sample_rate >> 4);
+  si[12] = (uint8_t)(((sample_rate & 0xF) << 4) | ((channels - 1) << 1) | ((bps - 1) >> 4));
+  si[13] = (uint8_t)(((bps - 1) & 0xF) << 4);
+  // MD5 zero
+  uint8_t* vc = o + 42;
+  const uint32_t vlen = (uint32_t)(sizeof(kVendor) - 1);
+  const uint32_t blen = 4 + vlen + 4;
+  vc[0] = 0x84;  // last | VORBIS_COMMENT
+  vc[1] = (uint8_t)(blen >> 16); vc[2] = (uint8_t)(blen >> 8); vc[3] = (uint8_t)blen;
+  vc[4] = (uint8_t)vlen; vc[5] = (uint8_t)(vlen >> 8); vc[6] = (uint8_t)(vlen >> 16); vc[7] = (uint8_t)(vlen >> 24);
+  memcpy(vc + 8, kVendor, vlen);
+  memset(vc + 8 + vlen, 0, 4);
+  return FRA_OK;  // 42 + 4 + 40 = 86 bytes
+}
+
+int fra_synth_raster(fra_ctx* ctx, int32_t kind, uint64_t seed, int32_t bands, int32_t height, int32_t width,
+                     void* dev_out) {
+  if (!ctx || !dev_out || bands < 1 || height < 1 || width < 1 || (kind != 3 && kind != 4 && kind != 5))
+    return set_err(FRA_E_INVALID, "bad synth arguments");
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(launch_synth(kind, seed, bands, height, width, dev_out, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return FRA_OK;
+}
+
+int fra_device_alloc(fra_ctx* ctx, uint64_t bytes, void** p) {
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(hipMalloc(p, bytes ? bytes : 1));
+  return FRA_OK;
+}
+int fra_device_free(fra_ctx* ctx, void* p) {
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(hipFree(p));
+  return FRA_OK;
+}
+int fra_memcpy_d2h(fra_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return FRA_OK;
+}
+int fra_memcpy_h2d(fra_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return FRA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,179 @@
+// fra_internal.h -- device-side data layout of the MI355X FLAC raster encoder (product code).
+//
+// The encode path replaces the pyflac/libFLAC call at src/flac_raster/converter.py:139-154 and
+// src/flac_raster/spatial_encoder.py:291-304 of the reference.  One "stream" = one FLAC stream =
+// one reference encode unit (a streaming/spatial tile, or the whole raster in the standard format).
+// One "frame" = blocksize (4096) consecutive samples of every channel of a stream.
+// One "subframe" = one channel of one frame (the unit of the analysis kernel).
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define FRA_HD __host__ __device__ inline
+#else
+#define FRA_HD inline
+#endif
+
+namespace fra {
+
+enum SrcType : int32_t { ST_U8 = 0, ST_I8, ST_U16, ST_I16, ST_U32, ST_I32, ST_F32, ST_F64 };
+
+constexpr int kMaxBlock = 4096;   // samples per frame handled by one workgroup (reference uses 4096)
+constexpr int kThreads = 256;     // 4 waves; each thread owns 16 consecutive samples
+constexpr int kChunk = 16;        // samples per thread (also the FRA-1 autocorrelation chunk)
+constexpr int kMaxLpc = 12;
+constexpr int kMaxPart = 64;      // 2^6 partitions (level 6-8 max partition order)
+constexpr int kMaxWin = 6;        // subdivide_tukey(3): 1 + 2 + 3 windows
+constexpr int kMaxModels = 5 + kMaxLpc + (kMaxWin - 1);  // fixed 0..4, window-0 orders, one per extra window
+
+// libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
+struct LevelCfg {
+  int32_t max_lpc, max_porder, nsub;
+};
+FRA_HD LevelCfg level_cfg(int level) {
+  switch (level < 0 ? 0 : (level > 8 ? 8 : level)) {
+    case 0: case 1: case 2: return {0, 3, 0};
+    case 3: return {6, 4, 1};
+    case 4: return {8, 4, 1};
+    case 5: return {8, 5, 1};
+    case 6: return {8, 6, 2};
+    case 7: return {12, 6, 2};
+    default: return {12, 6, 3};
+  }
+}
+FRA_HD int num_windows(int nsub) {
+  int c = nsub > 0 ? 1 : 0;
+  for (int m = 2; m <= nsub; m++) c += m;
+  return c;
+}
+// qlp coefficient precision: libFLAC's automatic rule (qlp_coeff_precision = 0 at every level)
+FRA_HD int qlp_precision(int bps, int bs) {
+  if (bps < 16) { int p = 2 + bps / 2; return p < 5 ? 5 : p; }
+  if (bps == 16) {
+    if (bs <= 192) return 7;
+    if (bs <= 384) return 8;
+    if (bs <= 576) return 9;
+    if (bs <= 1152) return 10;
+    if (bs <= 2304) return 11;
+    if (bs <= 4608) return 12;
+    return 13;
+  }
+  if (bs <= 384) return 13;
+  if (bs <= 1152) return 14;
+  return 15;
+}
+FRA_HD int max_porder(int n, int o, int cap) {
+  int p = 0;
+  while (p < cap && ((n >> (p + 1)) << (p + 1)) == n && (n >> (p + 1)) > o) p++;
+  return p;
+}
+
+// RFC 9639 frame-header code tables
+FRA_HD int bs_code(int bs, int* extra_bits) {
+  *extra_bits = 0;
+  if (bs == 192) return 1;
+  if (bs == 576) return 2;
+  if (bs == 1152) return 3;
+  if (bs == 2304) return 4;
+  if (bs == 4608) return 5;
+  for (int c = 8; c <= 15; c++)
+    if (bs == (256 << (c - 8))) return c;
+  if (bs <= 256) { *extra_bits = 8; return 6; }
+  *extra_bits = 16;
+  return 7;
+}
+FRA_HD int sr_code(int sr, int* extra_bits, int* extra_val) {
+  *extra_bits = 0;
+  *extra_val = 0;
+  switch (sr) {
+    case 88200: return 1;
+    case 176400: return 2;
+    case 192000: return 3;
+    case 8000: return 4;
+    case 16000: return 5;
+    case 22050: return 6;
+    case 24000: return 7;
+    case 32000: return 8;
+    case 44100: return 9;
+    case 48000: return 10;
+    case 96000: return 11;
+  }
+  if (sr % 1000 == 0 && sr / 1000 <= 255) { *extra_bits = 8; *extra_val = sr / 1000; return 12; }
+  if (sr <= 65535) { *extra_bits = 16; *extra_val = sr; return 13; }
+  if (sr % 10 == 0 && sr / 10 <= 65535) { *extra_bits = 16; *extra_val = sr / 10; return 14; }
+  return 0;
+}
+FRA_HD int bps_code(int bps) {
+  switch (bps) {
+    case 8: return 1;
+    case 12: return 2;
+    case 16: return 4;
+    case 20: return 5;
+    case 24: return 6;
+    case 32: return 7;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- device job description
+struct StreamDev {
+  int64_t base_off;      // element offset of (band 0, window row 0, window col 0)
+  int64_t band_stride;   // elements between bands (channels)
+  int64_t row_stride;    // elements between rows
+  int64_t col_stride;    // elements between pixels of a row
+  int32_t width, height; // window
+  int32_t channels;
+  int32_t bps;           // FLAC bits per sample: 16 or 32
+  int32_t norm;          // 0 = samples are already audio ints; 16 / 24 = normalize_to_audio(bps)
+  int32_t sample_rate;
+  int32_t first_frame, nframes;
+  int64_t nsamples;      // per channel (= width*height)
+};
+
+struct FrameDev {
+  int32_t stream;
+  int32_t index;   // frame number within its stream
+  int32_t n;       // block size of this frame
+  int32_t win;     // window-table index (one table set per distinct block size)
+  int32_t row0, col0;  // window-relative pixel position of sample 0
+};
+
+struct NormDev {       // per stream, filled on device
+  unsigned long long mnkey, mxkey;  // ordered-key min/max (NaN excluded)
+  double mn, mx, range;             // normalize_to_audio parameters (normalization.py:148-159)
+};
+
+// One analysed subframe (FRA-1 decision), written by k_analyze, read by k_frame_bytes/k_pack.
+struct SfDesc {
+  uint32_t bits;      // exact subframe size in bits
+  uint8_t type;       // 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC
+  uint8_t order;
+  uint8_t wasted;
+  uint8_t sbps;       // sample bits after wasted-bit shift (CONSTANT: stream bps)
+  uint8_t porder;
+  uint8_t method;     // 0 RICE (4-bit params), 1 RICE2 (5-bit)
+  uint8_t precision;
+  int8_t shift;
+  int32_t cval;       // CONSTANT value
+  int32_t coef[kMaxLpc];
+  uint8_t k[kMaxPart];
+};
+
+struct JobArgs {
+  const void* raster;
+  const StreamDev* streams;
+  const FrameDev* frames;
+  NormDev* norm;
+  const float* win;        // [ntables][nwin][blocksize]
+  SfDesc* sf;              // [nframes_total][cmax]
+  unsigned long long* frame_bytes;  // [nframes_total + 1] (last = 0)
+  unsigned long long* frame_off;  // [nframes_total + 1] exclusive scan of frame_bytes
+  uint8_t* out;            // concatenated frames
+  int32_t nframes_total;
+  int32_t cmax;
+  int32_t blocksize;
+  int32_t level;
+  int32_t nwin;
+};
+
+}  // namespace fra

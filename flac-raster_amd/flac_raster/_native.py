@@ -1,0 +1,299 @@
+"""ctypes binding of ``libflac_raster_amd.so`` (C ABI: ``include/flac_raster_amd.h``).
+
+This is the only compute path of the package: there is no CPU fallback.  If the library is
+missing, or no GPU is visible, every encode call raises :class:`NativeUnavailable` loudly.
+The library is built in-tree by ``flac-raster_amd/csrc/Makefile`` (``__graft_entry__.build()``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libflac_raster_amd.so"
+_lib = None
+_lock = threading.Lock()
+
+DTYPE_CODES = {
+    np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16): 3,
+    np.dtype(np.uint32): 4, np.dtype(np.int32): 5, np.dtype(np.float32): 6, np.dtype(np.float64): 7,
+}
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP extension is not built or no MI355X (gfx950) device is visible."""
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class Window(C.Structure):
+    _fields_ = [("row_off", C.c_int32), ("col_off", C.c_int32), ("height", C.c_int32), ("width", C.c_int32)]
+
+
+class Job(C.Structure):
+    _fields_ = [
+        ("raster", C.c_void_p), ("raster_on_device", C.c_int32), ("dtype", C.c_int32), ("channels", C.c_int32),
+        ("band_stride", C.c_int64), ("row_stride", C.c_int64), ("col_stride", C.c_int64),
+        ("windows", C.POINTER(Window)), ("nwindows", C.c_int32), ("level", C.c_int32), ("blocksize", C.c_int32),
+        ("norm", C.c_int32), ("sample_rate", C.c_int32),
+    ]
+
+
+class StreamInfo(C.Structure):
+    _fields_ = [
+        ("offset", C.c_uint64), ("frame_bytes", C.c_uint64), ("data_min", C.c_double), ("data_max", C.c_double),
+        ("sample_rate", C.c_int32), ("bps", C.c_int32), ("channels", C.c_int32), ("nframes", C.c_int32),
+    ]
+
+
+EXPORTS = [
+    "fra_last_error", "fra_abi_version", "fra_device_count", "fra_free", "fra_ctx_create", "fra_ctx_destroy",
+    "fra_plan_create", "fra_plan_set_raster", "fra_plan_execute", "fra_plan_sync", "fra_plan_result",
+    "fra_plan_download", "fra_plan_device_output", "fra_plan_enable_timing", "fra_plan_timing",
+    "fra_plan_destroy", "fra_encode", "fra_stream_header", "fra_synth_raster", "fra_device_alloc",
+    "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d",
+]
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def load():
+    """Load the shared library (no GPU needed just to load it)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not _LIB_PATH.exists():
+            raise NativeUnavailable(
+                f"{_LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C flac-raster_amd/csrc)")
+        L = C.CDLL(str(_LIB_PATH))
+        vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
+        L.fra_last_error.restype = C.c_char_p
+        L.fra_abi_version.restype = C.c_int
+        L.fra_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.fra_free.argtypes = [vp]
+        L.fra_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+        L.fra_ctx_destroy.argtypes = [vp]
+        L.fra_plan_create.argtypes = [vp, C.POINTER(Job), C.POINTER(vp)]
+        L.fra_plan_set_raster.argtypes = [vp, vp, i32]
+        L.fra_plan_execute.argtypes = [vp]
+        L.fra_plan_sync.argtypes = [vp]
+        L.fra_plan_result.argtypes = [vp, C.POINTER(StreamInfo), C.POINTER(u64)]
+        L.fra_plan_download.argtypes = [vp, vp, u64]
+        L.fra_plan_device_output.argtypes = [vp, C.POINTER(vp), C.POINTER(u64)]
+        L.fra_plan_enable_timing.argtypes = [vp, i32]
+        L.fra_plan_timing.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(i32)]
+        L.fra_plan_destroy.argtypes = [vp]
+        L.fra_encode.argtypes = [C.c_int, C.POINTER(Job), C.POINTER(vp), C.POINTER(u64), C.POINTER(StreamInfo)]
+        L.fra_stream_header.argtypes = [vp, i32, i32, i32, i32]
+        L.fra_synth_raster.argtypes = [vp, i32, u64, i32, i32, i32, vp]
+        L.fra_device_alloc.argtypes = [vp, u64, C.POINTER(vp)]
+        L.fra_device_free.argtypes = [vp, vp]
+        L.fra_memcpy_d2h.argtypes = [vp, vp, vp, u64]
+        L.fra_memcpy_h2d.argtypes = [vp, vp, vp, u64]
+        _lib = L
+        return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load().fra_last_error()
+        raise NativeError(f"flac_raster_amd error {rc}: {msg.decode() if msg else ''}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    load().fra_device_count(C.byref(n))
+    return n.value
+
+
+def stream_header(channels: int, bps: int, sample_rate: int, blocksize: int = 4096) -> bytes:
+    buf = (C.c_uint8 * 86)()
+    _check(load().fra_stream_header(buf, channels, bps, sample_rate, blocksize))
+    return bytes(buf)
+
+
+class Context:
+    """One HIP device + stream (``fra_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        if device_count() == 0:
+            raise NativeUnavailable("no HIP device visible: the flac_raster encoder requires an MI355X (gfx950)")
+        h = C.c_void_p()
+        _check(L.fra_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            load().fra_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        _check(load().fra_device_alloc(self.h, nbytes, C.byref(p)))
+        return p.value
+
+    def free(self, ptr: int):
+        _check(load().fra_device_free(self.h, C.c_void_p(ptr)))
+
+    def h2d(self, dev: int, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        _check(load().fra_memcpy_h2d(self.h, C.c_void_p(dev), a.ctypes.data_as(C.c_void_p), a.nbytes))
+
+    def d2h(self, arr: np.ndarray, dev: int):
+        _check(load().fra_memcpy_d2h(self.h, arr.ctypes.data_as(C.c_void_p), C.c_void_p(dev), arr.nbytes))
+
+    def synth(self, kind: int, seed: int, bands: int, height: int, width: int, dev_out: int):
+        _check(load().fra_synth_raster(self.h, kind, seed, bands, height, width, C.c_void_p(dev_out)))
+
+
+class Plan:
+    """Device workspace for one job (``fra_plan``): windows of one raster -> FLAC frame streams."""
+
+    def __init__(self, ctx: Context, raster_ptr: Optional[int], on_device: bool, dtype: np.dtype, channels: int,
+                 strides: Tuple[int, int, int], windows: Sequence[Tuple[int, int, int, int]], level: int = 5,
+                 blocksize: int = 4096, norm: int = 16, sample_rate: int = 0, keepalive=None):
+        L = load()
+        self.ctx = ctx
+        self.nwin = len(windows)
+        self._wins = (Window * max(1, self.nwin))(*[Window(*w) for w in windows])
+        self._keep = keepalive
+        job = Job()
+        job.raster = C.c_void_p(raster_ptr) if raster_ptr else None
+        job.raster_on_device = 1 if on_device else 0
+        job.dtype = DTYPE_CODES[np.dtype(dtype)]
+        job.channels = channels
+        job.band_stride, job.row_stride, job.col_stride = strides
+        job.windows = self._wins
+        job.nwindows = self.nwin
+        job.level = level
+        job.blocksize = blocksize
+        job.norm = norm
+        job.sample_rate = sample_rate
+        h = C.c_void_p()
+        _check(L.fra_plan_create(ctx.h, C.byref(job), C.byref(h)))
+        self.h = h
+
+    def set_raster(self, ptr: int, on_device: bool, keepalive=None):
+        self._keep = keepalive
+        _check(load().fra_plan_set_raster(self.h, C.c_void_p(ptr), 1 if on_device else 0))
+
+    def execute(self):
+        _check(load().fra_plan_execute(self.h))
+
+    def sync(self):
+        _check(load().fra_plan_sync(self.h))
+
+    def result(self) -> Tuple[List[StreamInfo], int]:
+        infos = (StreamInfo * max(1, self.nwin))()
+        total = C.c_uint64()
+        _check(load().fra_plan_result(self.h, infos, C.byref(total)))
+        return list(infos)[: self.nwin], total.value
+
+    def download(self) -> Tuple[List[StreamInfo], bytes]:
+        infos, total = self.result()
+        buf = np.empty(max(1, total), dtype=np.uint8)
+        _check(load().fra_plan_download(self.h, buf.ctypes.data_as(C.c_void_p), total))
+        return infos, buf[:total].tobytes()
+
+    def device_output(self) -> Tuple[int, int]:
+        p, cap = C.c_void_p(), C.c_uint64()
+        _check(load().fra_plan_device_output(self.h, C.byref(p), C.byref(cap)))
+        return p.value, cap.value
+
+    def enable_timing(self, on: bool = True):
+        _check(load().fra_plan_enable_timing(self.h, 1 if on else 0))
+
+    def timing(self) -> Tuple[List[float], int]:
+        ms = (C.c_float * 4)()
+        n = C.c_int32()
+        _check(load().fra_plan_timing(self.h, ms, C.byref(n)))
+        return list(ms), n.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().fra_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx = {}
+
+
+def default_context(device: int = 0) -> Context:
+    with _lock:
+        ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _default_ctx[device] = ctx
+    return ctx
+
+
+def encode_windows(raster: np.ndarray, windows, level: int = 5, blocksize: int = 4096, norm: int = 16,
+                   sample_rate: int = 0, device: int = 0):
+    """Encode windows of a band-planar host raster ``(B, H, W)`` (or ``(H, W)``).
+
+    Returns ``(infos, frames_bytes)``: ``frames_bytes`` holds every window's FLAC frames
+    concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.
+    """
+    a = np.ascontiguousarray(raster)
+    if a.ndim == 2:
+        a = a[None]
+    B, H, W = a.shape
+    ctx = default_context(device)
+    plan = Plan(ctx, a.ctypes.data, False, a.dtype, B, (H * W, W, 1), windows, level, blocksize, norm,
+                sample_rate, keepalive=a)
+    try:
+        plan.execute()
+        plan.sync()
+        return plan.download()
+    finally:
+        plan.close()
+
+
+def encode_interleaved(samples: np.ndarray, sample_rate: int, level: int = 5, blocksize: int = 4096,
+                       device: int = 0) -> Tuple[StreamInfo, bytes]:
+    """pyflac ``StreamEncoder.process(samples); finish()`` semantics: samples (N, C) int16/int32
+    already in the audio domain; bps = itemsize*8.  Returns (info, frames)."""
+    s = np.asarray(samples)
+    if s.ndim == 1:
+        s = s.reshape(-1, 1)
+    if s.dtype not in (np.int16, np.int32):
+        s = s.astype(np.int32)
+    s = np.ascontiguousarray(s)
+    N, Ch = s.shape
+    ctx = default_context(device)
+    # treat the (N, C) array as one raster row of N pixels with C interleaved bands
+    plan = Plan(ctx, s.ctypes.data, False, s.dtype, Ch, (1, N * Ch, Ch), [(0, 0, 1, N)] if N else [(0, 0, 0, 0)],
+                level, blocksize, 0, sample_rate, keepalive=s)
+    try:
+        plan.execute()
+        plan.sync()
+        infos, data = plan.download()
+        return infos[0], data
+    finally:
+        plan.close()

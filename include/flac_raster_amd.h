@@ -1,0 +1,142 @@
+/*
+ * flac_raster_amd.h -- C ABI of the MI355X (gfx950) FLAC raster encoder.
+ *
+ * This library replaces the encode half of the reference's pyflac/libFLAC boundary:
+ *
+ *   reference call site                                   what replaces it here
+ *   ---------------------------------------------------   -------------------------------------
+ *   pyflac.StreamEncoder(write_callback, sample_rate,     fra_encode() / fra_plan_*() with
+ *     compression_level, blocksize=4096)                  fra_job.norm = 0 (samples are already
+ *   encoder.process(audio); encoder.finish()              int16/int32 audio, pyflac semantics F3:
+ *     src/flac_raster/converter.py:139-154                bps = itemsize*8)
+ *     src/flac_raster/spatial_encoder.py:291-304
+ *     (pyflac 3.0.0 _Encoder.process/finish,
+ *      docs/sonos-pyflac.txt:1968-2014; libFLAC C ABI
+ *      FLAC__stream_encoder_new, set_..., init_stream,
+ *      process_interleaved/finish, :3205-3262)
+ *
+ *   normalize_to_audio(interleave(raster)) + the above,   fra_job.norm = 16 or 24: raw raster in,
+ *     once per encode unit (whole raster / tile)          per-window nanmin/nanmax + the float64
+ *     normalization.py:126-202, converter.py:93-154,      normalisation fused on the GPU
+ *     spatial_encoder.py:196-245, cli.py:553-622
+ *
+ * Output of an encode = the FLAC *frames* of every window's stream, concatenated in window order,
+ * plus per-stream info.  The 86-byte stream header (fLaC + STREAMINFO + VORBIS_COMMENT, F4 of
+ * SURVEY.md) is produced by fra_stream_header(); the Python host layer assembles headers, tags
+ * (mutagen-equivalent) and containers.
+ *
+ * Conventions: every function returns 0 on success or a negative fra_status; the message of the
+ * last failure on the calling thread is fra_last_error().  No C++ exception crosses this ABI.
+ * Library-allocated buffers are released with fra_free().  A context is bound to one HIP device
+ * and owns one HIP stream; plans are not thread-safe, distinct plans may run on distinct threads.
+ */
+#ifndef FLAC_RASTER_AMD_H
+#define FLAC_RASTER_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRA_ABI_VERSION 1
+
+#if defined(__GNUC__) || defined(__clang__)
+#define FRA_API __attribute__((visibility("default")))
+#else
+#define FRA_API
+#endif
+
+typedef enum {
+  FRA_OK = 0,
+  FRA_E_INVALID = -1,   /* bad argument */
+  FRA_E_HIP = -2,       /* HIP runtime error (message in fra_last_error) */
+  FRA_E_NODEVICE = -3,  /* no usable gfx950 device */
+  FRA_E_NOMEM = -4,
+  FRA_E_STATE = -5      /* call out of order (e.g. result before execute) */
+} fra_status;
+
+/* dtype codes of the source samples (numpy names) */
+typedef enum {
+  FRA_U8 = 0, FRA_I8 = 1, FRA_U16 = 2, FRA_I16 = 3, FRA_U32 = 4, FRA_I32 = 5, FRA_F32 = 6, FRA_F64 = 7
+} fra_dtype;
+
+/* one encode unit: a rasterio Window (cli.py:553-559 / spatial_encoder.py:110-121) */
+typedef struct {
+  int32_t row_off, col_off, height, width;
+} fra_window;
+
+typedef struct {
+  const void *raster;       /* element (band 0, row 0, col 0) */
+  int32_t raster_on_device; /* 1: device pointer on the context's GPU; 0: host memory (copied) */
+  int32_t dtype;            /* fra_dtype */
+  int32_t channels;         /* bands -> FLAC channels (1..8) */
+  int64_t band_stride;      /* elements between bands */
+  int64_t row_stride;       /* elements between rows */
+  int64_t col_stride;       /* elements between pixels of a row (1 planar, C interleaved) */
+  const fra_window *windows;
+  int32_t nwindows;
+  int32_t level;            /* FLAC compression level 0..8 (cli.py:60-62, default 5) */
+  int32_t blocksize;        /* samples per frame, 16..4096 (reference passes 4096) */
+  int32_t norm;             /* 0: samples already audio ints (pyflac path); 16 / 24: normalize_to_audio */
+  int32_t sample_rate;      /* 0: calculate_audio_params rule from window H*W (normalization.py:108-120) */
+} fra_job;
+
+typedef struct {
+  uint64_t offset;          /* byte offset of this stream's frames in the concatenated output */
+  uint64_t frame_bytes;     /* bytes of frames (header excluded) */
+  double data_min, data_max;/* normalize_to_audio params (NaN if all-NaN); 0/0 when norm == 0 */
+  int32_t sample_rate, bps, channels, nframes;
+} fra_stream_info;
+
+typedef struct fra_ctx fra_ctx;
+typedef struct fra_plan fra_plan;
+
+FRA_API const char *fra_last_error(void);
+FRA_API int fra_abi_version(void);
+FRA_API int fra_device_count(int *count);
+FRA_API void fra_free(void *p);
+
+FRA_API int fra_ctx_create(int device, fra_ctx **out);
+FRA_API void fra_ctx_destroy(fra_ctx *ctx);
+
+/* Plan = all device workspace for one job shape; execute enqueues only (no allocation/sync). */
+FRA_API int fra_plan_create(fra_ctx *ctx, const fra_job *job, fra_plan **out);
+FRA_API int fra_plan_set_raster(fra_plan *plan, const void *raster, int32_t raster_on_device);
+FRA_API int fra_plan_execute(fra_plan *plan);
+FRA_API int fra_plan_sync(fra_plan *plan);
+/* after sync: per-window info (array of plan's nwindows) and total output bytes */
+FRA_API int fra_plan_result(fra_plan *plan, fra_stream_info *infos, uint64_t *total_bytes);
+/* after sync: copy the concatenated frames (total_bytes) to host memory */
+FRA_API int fra_plan_download(fra_plan *plan, uint8_t *host_out, uint64_t capacity);
+/* device pointer of the concatenated frames (valid until the next execute / destroy) */
+FRA_API int fra_plan_device_output(fra_plan *plan, const uint8_t **dev_ptr, uint64_t *capacity);
+/* per-kernel timing with HIP events on the plan's stream: 0 minmax, 1 analyze, 2 frame-bytes+scan, 3 pack */
+FRA_API int fra_plan_enable_timing(fra_plan *plan, int32_t on);
+FRA_API int fra_plan_timing(fra_plan *plan, float *ms_sum4, int32_t *executes);
+FRA_API void fra_plan_destroy(fra_plan *plan);
+
+/* One-shot convenience: plan, execute, download.  *out (malloc'ed, fra_free) receives the
+ * concatenated frames; infos must hold job->nwindows entries. */
+FRA_API int fra_encode(int device, const fra_job *job, uint8_t **out, uint64_t *out_len, fra_stream_info *infos);
+
+/* fLaC + STREAMINFO(min=max blocksize, sizes 0, total samples 0, MD5 0) + VORBIS_COMMENT(vendor,
+ * 0 comments, last) -- the 86-byte libFLAC 1.4.3 stream header layout. */
+FRA_API int fra_stream_header(uint8_t *out86, int32_t channels, int32_t bps, int32_t sample_rate, int32_t blocksize);
+
+/* Synthetic rasters, generated on the device with integer-exact hashes so a
+ * host numpy mirror reproduces any window bit for bit.  kind: 3 = C3 DEM int16, 4 = C4 S2-like
+ * uint16 (4 bands), 5 = C5 reflectance float32.  dev_out: device buffer (bands, height, width). */
+FRA_API int fra_synth_raster(fra_ctx *ctx, int32_t kind, uint64_t seed, int32_t bands, int32_t height, int32_t width,
+                     void *dev_out);
+
+/* device memory helpers for hosts without a GPU array library */
+FRA_API int fra_device_alloc(fra_ctx *ctx, uint64_t bytes, void **dev_ptr);
+FRA_API int fra_device_free(fra_ctx *ctx, void *dev_ptr);
+FRA_API int fra_memcpy_d2h(fra_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+FRA_API int fra_memcpy_h2d(fra_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLAC_RASTER_AMD_H */

@@ -523,7 +523,7 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
   /* candidate list: FIXED 0..4 then LPC orders of window 0 then one LPC per extra window */
   int fmax = n - 1 < 4 ? n - 1 : 4;
   for (int o = 0; o <= fmax; o++) {
-    compute_residual(s, n, 2, o, NULL, 0, r);
+    if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue; /* 32-bps: residual outside int32 */
     int po, kk[256];
     uint64_t e = hdr + (uint64_t)o * sbps + residual_estimate(r, n, o, cfg->max_porder, &po, kk);
     if (btype < 0 || e < best_est) {

@@ -1,0 +1,176 @@
+"""GPU parity: the HIP encoder's FLAC frames must be byte-identical to the CPU oracle's
+(oracle/fr_oracle.c, FRA-1 rule) on the same inputs, and must decode bit-exactly to
+normalize_to_audio(input) -- the reference's compare_tiffs round-trip criterion at codec level.
+
+Inputs: the reference's own test rasters (tests/golden/*.tif), synthetic windows of the benchmark
+configurations (flac_raster.synth, identical on CPU and GPU), and edge cases (constant, NaN, inf,
+tiny/ragged windows, partial last frames, every compression level, 16- and 32-bps paths).
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle as O
+from flac_raster import _native as N
+from flac_raster.synth import synth_window
+from flac_raster.tiff import read_geotiff
+
+pytestmark = pytest.mark.gpu
+
+
+def _diag(got: bytes, exp: bytes, fb):
+    n = min(len(got), len(exp))
+    i = next((k for k in range(n) if got[k] != exp[k]), n)
+    f, acc = 0, 0
+    for f, b in enumerate(fb):
+        if acc + b > i:
+            break
+        acc += b
+    return f"len got {len(got)} exp {len(exp)}; first diff byte {i} (frame {f}, +{i - acc})"
+
+
+def check_windows(raster, windows, level, norm, blocksize=4096):
+    """Encode windows on the GPU and compare each stream with the oracle."""
+    infos, frames = N.encode_windows(raster, windows, level=level, norm=norm, blocksize=blocksize)
+    bps = 16 if norm == 16 else 24
+    total = 0
+    for (r0, c0, h, w), info in zip(windows, infos):
+        tile = raster[:, r0:r0 + h, c0:c0 + w]
+        inter = tile.transpose(1, 2, 0).reshape(-1, tile.shape[0])
+        audio, mn, mx = O.normalize(inter, bps)
+        sr = O.sample_rate_for_pixels(h * w)
+        assert info.sample_rate == sr
+        assert np.array_equal(np.array([info.data_min, info.data_max]), np.array([mn, mx]), equal_nan=True)
+        exp, fb, _ = O.encode(audio, sr, level=level, blocksize=blocksize, with_header=False, return_info=True)
+        got = frames[info.offset: info.offset + info.frame_bytes]
+        assert got == exp, f"window {(r0, c0, h, w)} level {level}: " + _diag(got, exp, fb)
+        if h * w:
+            hdr = O.stream_header(tile.shape[0], 16 if norm == 16 else 32, sr, blocksize)
+            dec, _, _, _ = O.decode(hdr + got)
+            assert np.array_equal(dec, audio.astype(np.int32))
+        total += len(got)
+    return total
+
+
+def tiles(H, W, t):
+    return [(r, c, min(t, H - r), min(t, W - c)) for r in range(0, H, t) for c in range(0, W, t)]
+
+
+def test_device_visible():
+    assert N.device_count() >= 1
+
+
+def test_stream_header_matches_oracle():
+    for ch, bps, sr in [(1, 16, 44100), (3, 16, 44100), (4, 16, 48000), (8, 32, 44100), (2, 32, 192000)]:
+        assert N.stream_header(ch, bps, sr, 4096) == O.stream_header(ch, bps, sr, 4096)
+
+
+@pytest.mark.parametrize("name", ["sample_rgb.tif", "sample_dem.tif", "sample_multispectral.tif"])
+@pytest.mark.parametrize("level", [0, 1, 3, 5, 6, 8])
+def test_reference_rasters_standard_format(golden_dir, name, level):
+    data, _ = read_geotiff(golden_dir / name)
+    B, H, W = data.shape
+    check_windows(data, [(0, 0, H, W)], level, 16)
+
+
+def test_sample_rgb_size_vs_libflac(golden_dir):
+    """-c 5 size vs the committed libFLAC 1.4.3 golden (178,857 frame bytes)."""
+    data, _ = read_geotiff(golden_dir / "sample_rgb.tif")
+    infos, frames = N.encode_windows(data, [(0, 0, 256, 256)], level=5, norm=16)
+    golden = (golden_dir / "sample_rgb.flac").read_bytes()
+    ratio = len(frames) / (len(golden) - 86)
+    assert ratio <= 1.02, ratio
+
+
+@pytest.mark.parametrize("level", [5])
+def test_sample_dem_spatial_tiles(golden_dir, level):
+    data, _ = read_geotiff(golden_dir / "sample_dem.tif")
+    check_windows(data, tiles(512, 512, 256), level, 16)
+
+
+def test_synthetic_s2_tiles_level5():
+    """C4-like: 4-band uint16, tile 1024 incl. ragged edge tiles (2832-sample last frame)."""
+    H = W = 1764  # 1024 + 740 -> full, 1024x740, 740x1024, 740x740 tiles
+    r = synth_window(4, 20260227, 4, H, W)
+    check_windows(r, tiles(H, W, 1024), 5, 16)
+
+
+@pytest.mark.parametrize("level", [0, 2, 4, 7])
+def test_synthetic_s2_levels(level):
+    r = synth_window(4, 7, 4, 300, 700)
+    check_windows(r, tiles(300, 700, 256), level, 16)
+
+
+def test_synthetic_dem_tiles():
+    r = synth_window(3, 11, 1, 1024, 1024)
+    check_windows(r, tiles(1024, 1024, 512), 5, 16)
+
+
+@pytest.mark.parametrize("level", [5, 8])
+def test_float32_24bit_path(level):
+    """C5-like: 8-band float32 -> int32 audio -> 32-bps FLAC."""
+    r = synth_window(5, 3, 8, 512, 512)
+    check_windows(r, tiles(512, 512, 256), level, 24)
+
+
+@pytest.mark.parametrize("dtype", ["uint8", "int8", "uint16", "int16", "uint32", "int32", "float32", "float64"])
+def test_all_dtypes(dtype):
+    rng = np.random.default_rng(abs(hash(dtype)) % 1000)
+    base = synth_window(4, 5, 3, 200, 300).astype(np.float64)
+    if dtype.startswith("float"):
+        r = (base / 1000.0).astype(dtype)
+    else:
+        info = np.iinfo(dtype)
+        r = np.clip(base - 1000 + (info.min + info.max) // 2, info.min, info.max).astype(dtype)
+    for norm in (16, 24):
+        check_windows(r, tiles(200, 300, 128), 5, norm)
+
+
+def test_edge_cases():
+    z = np.zeros((2, 64, 64), np.uint16)
+    check_windows(z, [(0, 0, 64, 64)], 5, 16)  # constant -> all -32767, CONSTANT subframes
+    r = synth_window(4, 9, 2, 97, 131)
+    wins = [(0, 0, 1, 1), (0, 0, 3, 5), (5, 7, 1, 131 - 7), (10, 0, 87, 1), (0, 0, 97, 131), (40, 50, 57, 81)]
+    check_windows(r, wins, 5, 16)
+    f = synth_window(5, 9, 3, 64, 80)
+    f[0, ::7, ::3] = np.nan
+    f[1, 5, 5] = np.inf
+    check_windows(f, [(0, 0, 64, 80), (0, 0, 32, 40)], 5, 16)
+    check_windows(f, [(0, 0, 64, 80)], 8, 24)
+    allnan = np.full((1, 40, 40), np.nan, np.float32)
+    check_windows(allnan, [(0, 0, 40, 40)], 5, 16)
+
+
+def test_small_blocksizes():
+    r = synth_window(4, 2, 2, 100, 100)
+    for bs in (16, 192, 1000, 1152, 4096):
+        check_windows(r, [(0, 0, 100, 100)], 5, 16, blocksize=bs)
+
+
+def test_interleaved_pyflac_path(golden_dir):
+    """pyflac StreamEncoder semantics: pre-normalised int16/int32 audio in."""
+    data, _ = read_geotiff(golden_dir / "sample_rgb.tif")
+    inter = data.transpose(1, 2, 0).reshape(-1, 3)
+    audio, _, _ = O.normalize(inter, 16)
+    info, frames = N.encode_interleaved(audio, 44100, level=5)
+    assert frames == O.encode(audio, 44100, level=5, with_header=False)
+    a32 = (audio.astype(np.int32) * 255)
+    info, frames = N.encode_interleaved(a32, 44100, level=5)
+    assert frames == O.encode(a32, 44100, level=5, with_header=False)
+    assert info.bps == 32
+
+
+def test_synth_matches_numpy_mirror():
+    ctx = N.default_context(0)
+    for kind, bands, dt in [(3, 1, np.int16), (4, 4, np.uint16), (5, 8, np.float32)]:
+        H, W = 300, 520
+        dev = ctx.alloc(bands * H * W * np.dtype(dt).itemsize)
+        try:
+            ctx.synth(kind, 99, bands, H, W, dev)
+            got = np.empty((bands, H, W), dt)
+            ctx.d2h(got, dev)
+        finally:
+            ctx.free(dev)
+        exp = synth_window(kind, 99, bands, H, W)
+        assert np.array_equal(got, exp), kind
