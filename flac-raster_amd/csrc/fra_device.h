@@ -1,0 +1,461 @@
+// fra_device.h -- device helpers shared by the encode kernels (fra_analyze.hip, fra_kernels.hip).
+//
+// Every floating-point helper on the decision path evaluates exactly the op sequence of its
+// oracle counterpart in oracle/fr_oracle.c (compile with -ffp-contract=off; IEEE add/mul/div/fma
+// are correctly rounded on gfx950 and x86-64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fra_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace fra {
+
+// ---------------------------------------------------------------- ordered keys for nanmin/nanmax
+__device__ __forceinline__ unsigned long long okey(double v) {
+  unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double unkey(unsigned long long k) {
+  unsigned long long b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)b);
+}
+
+// ---------------------------------------------------------------- typed loads
+template <int SRC>
+__device__ __forceinline__ double load_f64(const void* base, int64_t e) {
+  if constexpr (SRC == ST_U8) return (double)((const uint8_t*)base)[e];
+  else if constexpr (SRC == ST_I8) return (double)((const int8_t*)base)[e];
+  else if constexpr (SRC == ST_U16) return (double)((const uint16_t*)base)[e];
+  else if constexpr (SRC == ST_I16) return (double)((const int16_t*)base)[e];
+  else if constexpr (SRC == ST_U32) return (double)((const uint32_t*)base)[e];
+  else if constexpr (SRC == ST_I32) return (double)((const int32_t*)base)[e];
+  else if constexpr (SRC == ST_F32) return (double)((const float*)base)[e];
+  else return ((const double*)base)[e];
+}
+template <int SRC>
+__device__ __forceinline__ int32_t load_raw_int(const void* base, int64_t e) {
+  if constexpr (SRC == ST_I16) return (int32_t)((const int16_t*)base)[e];
+  else if constexpr (SRC == ST_I32) return ((const int32_t*)base)[e];
+  else return 0;  // norm == 0 is only accepted for int16/int32 samples (fra_plan_create)
+}
+
+// ---------------------------------------------------------------- normalize_to_audio
+struct NormParams {
+  double mn, range, rcp, scale;
+  bool to16;
+  int mode;  // 0 raw ints, else normalise
+};
+__device__ __forceinline__ NormParams norm_params(const StreamDev& st, const NormDev& nd) {
+  NormParams p;
+  p.mode = st.norm;
+  p.to16 = st.norm == 16;
+  p.scale = st.norm == 16 ? 32767.0 : 8388607.0;
+  double mn, mx;
+  if (nd.mnkey == ~0ull) {  // no non-NaN value: nanmin/nanmax -> NaN
+    mn = __longlong_as_double(0x7FF8000000000000ll);
+    mx = mn;
+  } else {
+    mn = unkey(nd.mnkey);
+    mx = unkey(nd.mxkey);
+  }
+  p.mn = mn;
+  p.range = (mx <= mn) ? 1.0 : (mx - mn);  // normalization.py:154-159
+  p.rcp = 1.0 / p.range;
+  return p;
+}
+// t/range for the integer dtypes by Markstein's reciprocal refinement: bit-identical to the IEEE
+// quotient for every t = 2*(x-mn) in [0, 2R], R integer (exhaustively verified for R < 2^16 by
+// tools/verify_markstein.c; theorem-backed for 32-bit integers: no under/overflow is possible).
+__device__ __forceinline__ double div_markstein(double t, double b, double y) {
+  const double q0 = t * y;
+  const double r = fma(-q0, b, t);
+  return fma(r, y, q0);
+}
+// normalization.py:162-187, op order as numpy evaluates ((2.0*(x-mn))/R)-1.0, clip, NaN->0, *scale, trunc
+template <int SRC>
+__device__ __forceinline__ int32_t norm_sample(double x, const NormParams& p) {
+  double t = x - p.mn;
+  t = 2.0 * t;
+  if constexpr (SRC == ST_F32 || SRC == ST_F64) t = t / p.range;
+  else t = div_markstein(t, p.range, p.rcp);
+  t = t - 1.0;
+  if (t < -1.0) t = -1.0;
+  else if (t > 1.0) t = 1.0;
+  if (t != t) t = 0.0;
+  t = t * p.scale;
+  return p.to16 ? (int32_t)(int16_t)(int32_t)t : (int32_t)t;
+}
+template <int SRC>
+__device__ __forceinline__ int32_t fetch_sample(const void* base, int64_t e, const NormParams& np) {
+  if (np.mode == 0) return load_raw_int<SRC>(base, e);
+  return norm_sample<SRC>(load_f64<SRC>(base, e), np);
+}
+
+template <int SRC> struct RawType { using T = double; };
+template <> struct RawType<ST_U8> { using T = uint8_t; };
+template <> struct RawType<ST_I8> { using T = int8_t; };
+template <> struct RawType<ST_U16> { using T = uint16_t; };
+template <> struct RawType<ST_I16> { using T = int16_t; };
+template <> struct RawType<ST_U32> { using T = uint32_t; };
+template <> struct RawType<ST_I32> { using T = int32_t; };
+template <> struct RawType<ST_F32> { using T = float; };
+
+// Load channel c of frame fr into smp[0..n): lane-contiguous (coalesced) element reads; all of a
+// thread's 16 loads are issued before any is consumed (latency overlap), addresses advance
+// incrementally (no per-sample division or 64-bit multiply).  Returns per-thread OR / min / max.
+template <int SRC>
+__device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                               const NormParams& np, int32_t* smp, uint32_t& orv, int32_t& vmin,
+                                               int32_t& vmax) {
+  using T = typename RawType<SRC>::T;
+  constexpr int K = kMaxBlock / kThreads;
+  const T* src = (const T*)base;
+  const int n = fr.n, w = st.width, t = threadIdx.x;
+  int col = fr.col0 + t, row = fr.row0;
+  if (col >= w) {
+    const int q = (int)((unsigned)col / (unsigned)w);
+    row += q;
+    col -= q * w;
+  }
+  int64_t e = st.base_off + (int64_t)c * st.band_stride + (int64_t)row * st.row_stride + (int64_t)col * st.col_stride;
+  const int64_t step = (int64_t)kThreads * st.col_stride;
+  const int64_t wrap = st.row_stride - (int64_t)w * st.col_stride;
+  // address of sample 0 (valid whenever n >= 1): out-of-range lanes re-read it, so the loads are
+  // unconditional and the compiler can keep all K in flight
+  const int64_t e_first = st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride +
+                          (int64_t)fr.col0 * st.col_stride;
+  T raw[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    raw[k] = src[(t + k * kThreads < n) ? e : e_first];
+    col += kThreads;
+    e += step;
+    if (col >= w) {
+      if (w >= kThreads) { col -= w; e += wrap; }
+      else {
+        const int q = (int)((unsigned)col / (unsigned)w);
+        col -= q * w;
+        e += (int64_t)q * wrap;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = t + k * kThreads;
+    if (i < n) {
+      int32_t v;
+      if (np.mode == 0) v = (int32_t)raw[k];
+      else v = norm_sample<SRC>((double)raw[k], np);
+      smp[i] = v;
+      orv |= (uint32_t)v;
+      vmin = min(vmin, v);
+      vmax = max(vmax, v);
+    }
+  }
+}
+__device__ __forceinline__ void load_channel(int src, const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                             const NormParams& np, int32_t* smp, uint32_t& orv, int32_t& vmin,
+                                             int32_t& vmax) {
+  switch (src) {  // wave-uniform dispatch
+    case ST_U8: load_channel_t<ST_U8>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_I8: load_channel_t<ST_I8>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_U16: load_channel_t<ST_U16>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_I16: load_channel_t<ST_I16>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_U32: load_channel_t<ST_U32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_I32: load_channel_t<ST_I32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_F32: load_channel_t<ST_F32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    default: load_channel_t<ST_F64>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+  }
+}
+
+// ---------------------------------------------------------------- integer helpers
+__device__ __forceinline__ uint64_t zz64(int64_t r) {
+  return r >= 0 ? ((uint64_t)r << 1) : ((((uint64_t)(-(r + 1))) << 1) | 1u);
+}
+__device__ __forceinline__ uint32_t zz32(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
+__device__ __forceinline__ int bitlen64(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
+
+// Rice parameter estimate == oracle rice_pick: kc = bitlen(S / n) computed without
+// a division: kc = smallest k >= 0 with S < n*2^k, which is max(0, bitlen(S)-bitlen(n)) or one more.
+__device__ __forceinline__ uint64_t rice_est2(uint64_t n, uint64_t S, int k) {
+  const uint64_t lo = n * (uint64_t)((1u << k) - 1u);
+  const uint64_t tail = (2 * S > lo) ? ((2 * S - lo) >> (k + 1)) : 0;
+  return n * (uint64_t)(k + 1) + tail;
+}
+__device__ __forceinline__ void rice_pick(uint64_t n, uint64_t S, int& k_out, uint64_t& bits_out) {
+  const int a = bitlen64(S), b = bitlen64(n);
+  int kc = a > b ? a - b : 0;
+  if (S >= (n << kc)) kc++;
+  const int lo = kc - 2 < 0 ? 0 : kc - 2, hi = kc + 1 > 30 ? 30 : kc + 1;
+  uint64_t best = rice_est2(n, S, lo);
+  int bk = lo;
+  for (int k = lo + 1; k <= hi; k++) {
+    const uint64_t e = rice_est2(n, S, k);
+    if (e < best) { best = e; bk = k; }
+  }
+  k_out = bk;
+  bits_out = best;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  for (int off = 32; off >= 1; off >>= 1) v += shfl_xor_u64(v, off);
+  return v;
+}
+
+// ---------------------------------------------------------------- LPC analysis helpers
+// deterministic log2 -- same op sequence as oracle ora_det_log2
+__device__ inline double det_log2(double x) {
+  int e;
+  double m = frexp(x, &e);
+  m = m * 2.0;
+  e = e - 1;
+  const double t = (m - 1.0) / (m + 1.0);
+  const double t2 = t * t;
+  double sum = 0.0, p = t;
+  for (int k = 0; k < 12; k++) {
+    sum = sum + p / (double)(2 * k + 1);
+    p = p * t2;
+  }
+  return (double)e + 2.0 * sum * 1.4426950408889634;
+}
+__device__ inline int best_order_by_error(const double* err, int norders, int n, int overhead) {
+  double best = 0.0;
+  int bo = 1;
+  for (int o = 1; o <= norders; o++) {
+    const double e = err[o - 1];
+    double bps;
+    if (e > 0.0) {
+      bps = 0.5 * det_log2(0.5 * e / (double)n);
+      if (bps < 0.0) bps = 0.0;
+    } else if (e < 0.0) bps = 1e32;
+    else bps = 0.0;
+    const double bits = bps * (double)(n - o) + (double)(o * overhead);
+    if (o == 1 || bits < best) { best = bits; bo = o; }
+  }
+  return bo;
+}
+
+// Levinson-Durbin, same op sequence as oracle ora_levinson; loops unrolled to the
+// compile-time bound so the recursion state stays in registers.
+template <int MAXLAG>
+__device__ inline int levinson(const double* autoc, int max_order, double (*lp)[kMaxLpc], double* err_out) {
+  double lpc[MAXLAG];
+#pragma unroll
+  for (int j = 0; j < MAXLAG; j++) lpc[j] = 0.0;
+  double err = autoc[0];
+  int result = max_order;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < MAXLAG; i++) {
+    if (!done && i < max_order) {
+      double r = -autoc[i + 1];
+#pragma unroll
+      for (int j = 0; j < i; j++) r = r - lpc[j] * autoc[i - j];
+      r = r / err;
+      lpc[i] = r;
+#pragma unroll
+      for (int j = 0; j < (i >> 1); j++) {
+        const double tmp = lpc[j];
+        lpc[j] = lpc[j] + r * lpc[i - 1 - j];
+        lpc[i - 1 - j] = lpc[i - 1 - j] + r * tmp;
+      }
+      if (i & 1) lpc[i >> 1] = lpc[i >> 1] + lpc[i >> 1] * r;
+      err = err * (1.0 - r * r);
+#pragma unroll
+      for (int j = 0; j <= i; j++) lp[i][j] = -lpc[j];
+      err_out[i] = err;
+      if (!(err > 0.0)) {
+        result = (err == 0.0) ? i + 1 : i;
+        done = true;
+      }
+    }
+  }
+  return result;
+}
+
+__device__ __forceinline__ double rnd_half_away(double x) {
+  double t = trunc(x);
+  const double d = x - t;
+  if (d >= 0.5) t = t + 1.0;
+  else if (d <= -0.5) t = t - 1.0;
+  return t;
+}
+// qlp quantisation with error feedback; false if not representable
+template <int MAXLAG>
+__device__ inline bool quantize(const double* lp, int order, int precision, int32_t* q, int& shift_out) {
+  double cmax = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXLAG; j++) {
+    if (j < order) {
+      const double a = fabs(lp[j]);
+      if (a > cmax) cmax = a;
+    }
+  }
+  if (!(cmax > 0.0)) return false;
+  int e;
+  (void)frexp(cmax, &e);
+  int shift = precision - 1 - e;
+  if (shift > 15) shift = 15;
+  if (shift < 0) return false;
+  const int32_t qmax = (1 << (precision - 1)) - 1, qmin = -(1 << (precision - 1));
+  double errf = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXLAG; j++) {
+    if (j < order) {
+      errf = errf + ldexp(lp[j], shift);
+      const double qd = rnd_half_away(errf);
+      int32_t qi = (int32_t)qd;
+      if (qi > qmax) qi = qmax;
+      if (qi < qmin) qi = qmin;
+      errf = errf - (double)qi;
+      q[j] = qi;
+    } else {
+      q[j] = 0;
+    }
+  }
+  shift_out = shift;
+  return true;
+}
+
+// ---------------------------------------------------------------- residual evaluators
+// x[12 + jj] = sample i0 + jj; x[0..11] = the 12 preceding samples (0 before the block start).
+template <bool B32, int O>
+__device__ __forceinline__ int64_t fixed_res(const int32_t* x, int jj) {
+  const int b = 12 + jj;
+  if constexpr (B32) {
+    const int64_t s0 = x[b];
+    if constexpr (O == 0) return s0;
+    else if constexpr (O == 1) return s0 - (int64_t)x[b - 1];
+    else if constexpr (O == 2) return s0 - 2 * (int64_t)x[b - 1] + (int64_t)x[b - 2];
+    else if constexpr (O == 3) return s0 - 3 * (int64_t)x[b - 1] + 3 * (int64_t)x[b - 2] - (int64_t)x[b - 3];
+    else return s0 - 4 * (int64_t)x[b - 1] + 6 * (int64_t)x[b - 2] - 4 * (int64_t)x[b - 3] + (int64_t)x[b - 4];
+  } else {
+    const int32_t s0 = x[b];
+    if constexpr (O == 0) return s0;
+    else if constexpr (O == 1) return s0 - x[b - 1];
+    else if constexpr (O == 2) return s0 - 2 * x[b - 1] + x[b - 2];
+    else if constexpr (O == 3) return s0 - 3 * x[b - 1] + 3 * x[b - 2] - x[b - 3];
+    else return s0 - 4 * x[b - 1] + 6 * x[b - 2] - 4 * x[b - 3] + x[b - 4];
+  }
+}
+template <bool B32, int O>
+__device__ __forceinline__ int64_t lpc_res(const int32_t* x, int jj, const int32_t* q, int sh) {
+  const int b = 12 + jj;
+  if constexpr (B32) {
+    int64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < O; j++) sum += (int64_t)q[j] * (int64_t)x[b - 1 - j];
+    return (int64_t)x[b] - (sum >> sh);
+  } else {
+    int32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < O; j++) sum += q[j] * x[b - 1 - j];
+    return (int64_t)(x[b] - (sum >> sh));
+  }
+}
+// residual of sample jj for a runtime model (slow paths only)
+template <bool B32>
+__device__ __forceinline__ int64_t model_res(const int32_t* x, int jj, int type, int o, const int32_t* q, int sh) {
+  if (type == 2) {
+    switch (o) {
+      case 0: return fixed_res<B32, 0>(x, jj);
+      case 1: return fixed_res<B32, 1>(x, jj);
+      case 2: return fixed_res<B32, 2>(x, jj);
+      case 3: return fixed_res<B32, 3>(x, jj);
+      default: return fixed_res<B32, 4>(x, jj);
+    }
+  }
+  const int b = 12 + jj;
+  if constexpr (B32) {
+    int64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpc; j++)
+      if (j < o) sum += (int64_t)q[j] * (int64_t)x[b - 1 - j];
+    return (int64_t)x[b] - (sum >> sh);
+  } else {
+    int32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpc; j++)
+      if (j < o) sum += q[j] * x[b - 1 - j];
+    return (int64_t)(x[b] - (sum >> sh));
+  }
+}
+
+// ---------------------------------------------------------------- generic residual body
+// r = x[i] - ((sum_j q[j] * x[i-1-j]) >> sh), q[j] = 0 for j >= order; x[12 + jj] = sample i0 + jj
+template <bool B32, int MAXO>
+__device__ __forceinline__ int64_t gres(const int32_t* x, int jj, const int32_t* q, int sh) {
+  const int b = 12 + jj;
+  if constexpr (B32) {
+    int64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)x[b - 1 - j];
+    return (int64_t)x[b] - (sum >> sh);
+  } else {
+    int32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], x[b - 1 - j]);
+    return (int64_t)(x[b] - (sum >> sh));
+  }
+}
+// the same predictor read from the LDS sample array (slow path: irregular frames only)
+template <bool B32, int MAXO>
+__device__ __forceinline__ int64_t gres_lds(const int32_t* smp, int i, const int32_t* q, int sh) {
+  if constexpr (B32) {
+    int64_t sum = 0;
+    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[max(0, i - 1 - j)];
+    return (int64_t)smp[i] - (sum >> sh);
+  } else {
+    int32_t sum = 0;
+    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], smp[max(0, i - 1 - j)]);
+    return (int64_t)(smp[i] - (sum >> sh));
+  }
+}
+
+// ---------------------------------------------------------------- frame header (RFC 9639 9.1)
+__host__ __device__ inline int utf8_len(uint32_t v) {
+  if (v < 0x80) return 1;
+  if (v < 0x800) return 2;
+  if (v < 0x10000) return 3;
+  if (v < 0x200000) return 4;
+  if (v < 0x4000000) return 5;
+  return 6;
+}
+__device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameDev& fr) {
+  int bsx, srx, srv;
+  const int bc = bs_code(fr.n, &bsx);
+  const int sc = sr_code(st.sample_rate, &srx, &srv);
+  int p = 0;
+  h[p++] = 0xFF;
+  h[p++] = 0xF8;
+  h[p++] = (uint8_t)((bc << 4) | sc);
+  h[p++] = (uint8_t)(((st.channels - 1) << 4) | (bps_code(st.bps) << 1));
+  const uint32_t v = (uint32_t)fr.index;
+  const int nb = utf8_len(v);
+  if (nb == 1) h[p++] = (uint8_t)v;
+  else {
+    h[p++] = (uint8_t)(((0xFF00u >> nb) & 0xFF) | (v >> (6 * (nb - 1))));
+    for (int i = nb - 2; i >= 0; i--) h[p++] = (uint8_t)(0x80 | ((v >> (6 * i)) & 0x3F));
+  }
+  if (bsx == 8) h[p++] = (uint8_t)(fr.n - 1);
+  else if (bsx == 16) { h[p++] = (uint8_t)((fr.n - 1) >> 8); h[p++] = (uint8_t)(fr.n - 1); }
+  if (srx == 8) h[p++] = (uint8_t)srv;
+  else if (srx == 16) { h[p++] = (uint8_t)(srv >> 8); h[p++] = (uint8_t)srv; }
+  return p;
+}
+__device__ inline int frame_header_len(const StreamDev& st, const FrameDev& fr) {
+  int bsx, srx, srv;
+  bs_code(fr.n, &bsx);
+  sr_code(st.sample_rate, &srx, &srv);
+  return 4 + utf8_len((uint32_t)fr.index) + bsx / 8 + srx / 8 + 1;  // + CRC-8
+}
+
+}  // namespace fra

@@ -20,233 +20,9 @@
 // Numerics: compiled with -ffp-contract=off; every float/double expression on the decision path
 // is evaluated in exactly the order the oracle uses (IEEE add/mul/div are correctly rounded on
 // gfx950 and on x86-64, so identical op sequences give identical bits).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "fra_internal.h"
-
-#pragma clang fp contract(off)
+#include "fra_device.h"
 
 namespace fra {
-
-// ============================================================================ helpers
-__device__ __forceinline__ unsigned long long okey(double v) {
-  unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double unkey(unsigned long long k) {
-  unsigned long long b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
-  return __longlong_as_double((long long)b);
-}
-
-template <int SRC>
-__device__ __forceinline__ double load_f64(const void* base, int64_t e) {
-  if constexpr (SRC == ST_U8) return (double)((const uint8_t*)base)[e];
-  else if constexpr (SRC == ST_I8) return (double)((const int8_t*)base)[e];
-  else if constexpr (SRC == ST_U16) return (double)((const uint16_t*)base)[e];
-  else if constexpr (SRC == ST_I16) return (double)((const int16_t*)base)[e];
-  else if constexpr (SRC == ST_U32) return (double)((const uint32_t*)base)[e];
-  else if constexpr (SRC == ST_I32) return (double)((const int32_t*)base)[e];
-  else if constexpr (SRC == ST_F32) return (double)((const float*)base)[e];
-  else return ((const double*)base)[e];
-}
-template <int SRC>
-__device__ __forceinline__ int32_t load_raw_int(const void* base, int64_t e) {
-  if constexpr (SRC == ST_I16) return (int32_t)((const int16_t*)base)[e];
-  else if constexpr (SRC == ST_I32) return ((const int32_t*)base)[e];
-  else if constexpr (SRC == ST_U8) return (int32_t)((const uint8_t*)base)[e];
-  else if constexpr (SRC == ST_I8) return (int32_t)((const int8_t*)base)[e];
-  else if constexpr (SRC == ST_U16) return (int32_t)((const uint16_t*)base)[e];
-  else if constexpr (SRC == ST_U32) return (int32_t)((const uint32_t*)base)[e];
-  else return 0;
-}
-
-// normalize_to_audio for one value (normalization.py:162-187), op order as numpy evaluates it
-__device__ __forceinline__ int32_t norm_sample(double x, double mn, double range, double scale, bool to16) {
-  double t = x - mn;
-  t = 2.0 * t;
-  t = t / range;
-  t = t - 1.0;
-  if (t < -1.0) t = -1.0;
-  else if (t > 1.0) t = 1.0;
-  if (t != t) t = 0.0;
-  t = t * scale;
-  return to16 ? (int32_t)(int16_t)(int32_t)t : (int32_t)t;
-}
-
-struct NormParams {
-  double mn, range, scale;
-  bool to16;
-  int mode;  // 0 raw ints, else normalise
-};
-__device__ __forceinline__ NormParams norm_params(const StreamDev& st, const NormDev& nd) {
-  NormParams p;
-  p.mode = st.norm;
-  p.to16 = st.norm == 16;
-  p.scale = st.norm == 16 ? 32767.0 : 8388607.0;
-  double mn, mx;
-  if (nd.mnkey == ~0ull) {  // no non-NaN value: nanmin/nanmax -> NaN
-    mn = __longlong_as_double(0x7FF8000000000000ll);
-    mx = mn;
-  } else {
-    mn = unkey(nd.mnkey);
-    mx = unkey(nd.mxkey);
-  }
-  p.mn = mn;
-  p.range = (mx <= mn) ? 1.0 : (mx - mn);
-  return p;
-}
-
-template <int SRC>
-__device__ __forceinline__ int32_t fetch_sample(const void* base, int64_t e, const NormParams& np) {
-  if (np.mode == 0) return load_raw_int<SRC>(base, e);
-  return norm_sample(load_f64<SRC>(base, e), np.mn, np.range, np.scale, np.to16);
-}
-
-// element offset of sample i of channel c of frame fr
-__device__ __forceinline__ int64_t sample_elem(const StreamDev& st, const FrameDev& fr, int c, int i) {
-  int col = fr.col0 + i;
-  int row = fr.row0;
-  if (col >= st.width) {
-    int q = (unsigned)col / (unsigned)st.width;
-    row += q;
-    col -= q * st.width;
-  }
-  return st.base_off + (int64_t)c * st.band_stride + (int64_t)row * st.row_stride + (int64_t)col * st.col_stride;
-}
-
-__device__ __forceinline__ uint64_t zz64(int64_t r) {
-  return r >= 0 ? ((uint64_t)r << 1) : ((((uint64_t)(-(r + 1))) << 1) | 1u);
-}
-__device__ __forceinline__ int bitlen64(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
-
-// Rice parameter estimate, identical to oracle rice_pick/rice_est2
-__device__ __forceinline__ uint64_t rice_est2(uint64_t n, uint64_t S, int k) {
-  uint64_t lo = n * (uint64_t)((1u << k) - 1u);
-  uint64_t tail = (2 * S > lo) ? ((2 * S - lo) >> (k + 1)) : 0;
-  return n * (uint64_t)(k + 1) + tail;
-}
-__device__ __forceinline__ void rice_pick(uint64_t n, uint64_t S, int& k_out, uint64_t& bits_out) {
-  uint64_t mean = n ? S / n : 0;
-  int kc = bitlen64(mean);
-  int lo = kc - 2 < 0 ? 0 : kc - 2, hi = kc + 1 > 30 ? 30 : kc + 1;
-  uint64_t best = rice_est2(n, S, lo);
-  int bk = lo;
-  for (int k = lo + 1; k <= hi; k++) {
-    uint64_t e = rice_est2(n, S, k);
-    if (e < best) { best = e; bk = k; }
-  }
-  k_out = bk;
-  bits_out = best;
-}
-
-// 64-bit wave reductions via 32-bit halves
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-  for (int off = 32; off >= 1; off >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)v, off, 64);
-    uint32_t hi = __shfl_xor((uint32_t)(v >> 32), off, 64);
-    v += ((uint64_t)hi << 32) | lo;
-  }
-  return v;
-}
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  uint32_t lo = __shfl((uint32_t)v, src, 64);
-  uint32_t hi = __shfl((uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// deterministic log2 -- same op sequence as oracle ora_det_log2
-__device__ double det_log2(double x) {
-  int e;
-  double m = frexp(x, &e);
-  m = m * 2.0;
-  e = e - 1;
-  double t = (m - 1.0) / (m + 1.0);
-  double t2 = t * t;
-  double sum = 0.0, p = t;
-  for (int k = 0; k < 12; k++) {
-    sum = sum + p / (double)(2 * k + 1);
-    p = p * t2;
-  }
-  return (double)e + 2.0 * sum * 1.4426950408889634;
-}
-
-__device__ int best_order_by_error(const double* err, int norders, int n, int overhead) {
-  double best = 0.0;
-  int bo = 1;
-  for (int o = 1; o <= norders; o++) {
-    double e = err[o - 1], bps;
-    if (e > 0.0) {
-      bps = 0.5 * det_log2(0.5 * e / (double)n);
-      if (bps < 0.0) bps = 0.0;
-    } else if (e < 0.0) bps = 1e32;
-    else bps = 0.0;
-    double bits = bps * (double)(n - o) + (double)(o * overhead);
-    if (o == 1 || bits < best) { best = bits; bo = o; }
-  }
-  return bo;
-}
-
-// Levinson-Durbin -- same op sequence as oracle ora_levinson
-__device__ int levinson(const double* autoc, int max_order, double (*lp)[kMaxLpc], double* err_out) {
-  double lpc[kMaxLpc];
-  double err = autoc[0];
-  for (int i = 0; i < max_order; i++) {
-    double r = -autoc[i + 1];
-    for (int j = 0; j < i; j++) r = r - lpc[j] * autoc[i - j];
-    r = r / err;
-    lpc[i] = r;
-    int j;
-    for (j = 0; j < (i >> 1); j++) {
-      double tmp = lpc[j];
-      lpc[j] = lpc[j] + r * lpc[i - 1 - j];
-      lpc[i - 1 - j] = lpc[i - 1 - j] + r * tmp;
-    }
-    if (i & 1) lpc[j] = lpc[j] + lpc[j] * r;
-    err = err * (1.0 - r * r);
-    for (j = 0; j <= i; j++) lp[i][j] = -lpc[j];
-    err_out[i] = err;
-    if (err > 0.0) continue;
-    return err == 0.0 ? i + 1 : i;
-  }
-  return max_order;
-}
-
-__device__ __forceinline__ double rnd_half_away(double x) {
-  double t = trunc(x);
-  double d = x - t;
-  if (d >= 0.5) t = t + 1.0;
-  else if (d <= -0.5) t = t - 1.0;
-  return t;
-}
-
-// qlp quantisation with error feedback; returns false if not representable
-__device__ bool quantize(const double* lp, int order, int precision, int32_t* q, int& shift_out) {
-  double cmax = 0.0;
-  for (int j = 0; j < order; j++) {
-    double a = fabs(lp[j]);
-    if (a > cmax) cmax = a;
-  }
-  if (!(cmax > 0.0)) return false;
-  int e;
-  (void)frexp(cmax, &e);
-  int shift = precision - 1 - e;
-  if (shift > 15) shift = 15;
-  if (shift < 0) return false;
-  int32_t qmax = (1 << (precision - 1)) - 1, qmin = -(1 << (precision - 1));
-  double errf = 0.0;
-  for (int j = 0; j < order; j++) {
-    errf = errf + ldexp(lp[j], shift);
-    double qd = rnd_half_away(errf);
-    int32_t qi = (int32_t)qd;
-    if (qi > qmax) qi = qmax;
-    if (qi < qmin) qi = qmin;
-    errf = errf - (double)qi;
-    q[j] = qi;
-  }
-  shift_out = shift;
-  return true;
-}
 
 // ============================================================================ k_norm_init / k_minmax
 __global__ void k_norm_init(NormDev* nd, int nstreams) {
@@ -301,410 +77,6 @@ __global__ void __launch_bounds__(256) k_minmax(const void* raster, const Stream
       atomicMax(&nd[blockIdx.y].mxkey, kmax);
     }
   }
-}
-
-// ============================================================================ k_analyze
-// LDS layout (bytes): samples 16 KiB | windowed floats / partition sums 16.5 KiB | small tables
-struct AnalyzeSmem {
-  int32_t smp[kMaxBlock];
-  union {
-    float wf[kMaxBlock + 32];
-    unsigned long long psum[kMaxModels][kMaxPart];
-    unsigned long long esum[kMaxPart][3];
-  } u;
-  double red[4][kMaxLpc + 1];
-  double autoc[kMaxLpc + 1];
-  double lp[kMaxLpc][kMaxLpc];
-  double err[kMaxLpc];
-  int32_t mcoef[kMaxModels][kMaxLpc];
-  int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
-  unsigned long long mest[kMaxModels];
-  uint32_t ired[4][3];
-  int32_t kpart[kMaxPart];
-  int32_t nord, olo, ohi, winner;
-};
-
-// residual for sample at register position jj (x[12 + jj] is the sample), model m
-template <bool B32>
-__device__ __forceinline__ int64_t model_residual(const int32_t* x, int jj, int type, int o, const int32_t* q, int shift) {
-  const int b = 12 + jj;
-  if (type == 2) {
-    if constexpr (B32) {
-      int64_t s0 = x[b], s1 = x[b - 1], s2 = x[b - 2], s3 = x[b - 3], s4 = x[b - 4];
-      switch (o) {
-        case 0: return s0;
-        case 1: return s0 - s1;
-        case 2: return s0 - 2 * s1 + s2;
-        case 3: return s0 - 3 * s1 + 3 * s2 - s3;
-        default: return s0 - 4 * s1 + 6 * s2 - 4 * s3 + s4;
-      }
-    } else {
-      int32_t s0 = x[b], s1 = x[b - 1], s2 = x[b - 2], s3 = x[b - 3], s4 = x[b - 4];
-      switch (o) {
-        case 0: return s0;
-        case 1: return s0 - s1;
-        case 2: return s0 - 2 * s1 + s2;
-        case 3: return s0 - 3 * s1 + 3 * s2 - s3;
-        default: return s0 - 4 * s1 + 6 * s2 - 4 * s3 + s4;
-      }
-    }
-  } else {
-    if constexpr (B32) {
-      int64_t sum = 0;
-#pragma unroll
-      for (int j = 0; j < kMaxLpc; j++)
-        if (j < o) sum += (int64_t)q[j] * (int64_t)x[b - 1 - j];
-      return (int64_t)x[b] - (sum >> shift);
-    } else {
-      int32_t sum = 0;
-#pragma unroll
-      for (int j = 0; j < kMaxLpc; j++)
-        if (j < o) sum += q[j] * x[b - 1 - j];
-      return (int64_t)(x[b] - (sum >> shift));
-    }
-  }
-}
-
-template <int SRC, bool B32>
-__global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a) {
-  __shared__ AnalyzeSmem S;
-  const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const FrameDev fr = a.frames[g];
-  const StreamDev st = a.streams[fr.stream];
-  if (c >= st.channels) return;
-  const int n = fr.n;
-  const int bps = st.bps;
-  const LevelCfg cfg = level_cfg(a.level);
-  const NormParams np = norm_params(st, a.norm[fr.stream]);
-  SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
-
-  // ---- 1. load + normalise (coalesced: lane-contiguous samples)
-  uint32_t orv = 0;
-  int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-  for (int i = t; i < n; i += kThreads) {
-    int32_t v = fetch_sample<SRC>(a.raster, sample_elem(st, fr, c, i), np);
-    S.smp[i] = v;
-    orv |= (uint32_t)v;
-    vmin = min(vmin, v);
-    vmax = max(vmax, v);
-  }
-  for (int off = 32; off >= 1; off >>= 1) {
-    orv |= __shfl_xor(orv, off, 64);
-    vmin = min(vmin, __shfl_xor(vmin, off, 64));
-    vmax = max(vmax, __shfl_xor(vmax, off, 64));
-  }
-  if (lane == 0) { S.ired[wv][0] = orv; S.ired[wv][1] = (uint32_t)vmin; S.ired[wv][2] = (uint32_t)vmax; }
-  __syncthreads();
-  orv = S.ired[0][0] | S.ired[1][0] | S.ired[2][0] | S.ired[3][0];
-  vmin = min(min((int32_t)S.ired[0][1], (int32_t)S.ired[1][1]), min((int32_t)S.ired[2][1], (int32_t)S.ired[3][1]));
-  vmax = max(max((int32_t)S.ired[0][2], (int32_t)S.ired[1][2]), max((int32_t)S.ired[2][2], (int32_t)S.ired[3][2]));
-
-  // ---- 2. CONSTANT (3.2)
-  if (vmin == vmax) {
-    if (t == 0) {
-      d->type = 0; d->order = 0; d->wasted = 0; d->sbps = (uint8_t)bps; d->cval = vmin;
-      d->bits = 8u + (uint32_t)bps; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
-    }
-    return;
-  }
-  // ---- 3. wasted bits (3.3)
-  const int w = __builtin_ctz(orv);
-  const int sbps = bps - w;
-  if (w) {
-    __syncthreads();
-    for (int i = t; i < n; i += kThreads) S.smp[i] = S.smp[i] >> w;
-  }
-  const uint64_t hdr = 8u + (uint64_t)(w ? w : 0);
-  const uint64_t verb = hdr + (uint64_t)n * (uint64_t)sbps;
-  __syncthreads();
-
-  // register window: x[12 + jj] = sample 16t + jj, x[0..11] = the 12 preceding samples
-  int32_t x[12 + kChunk];
-  const int i0 = t * kChunk;
-#pragma unroll
-  for (int j = 0; j < 12 + kChunk; j++) {
-    int i = i0 - 12 + j;
-    x[j] = (i >= 0 && i < n) ? S.smp[i] : 0;
-  }
-
-  // ---- 4. model table: fixed orders
-  const int fmax = n - 1 < 4 ? n - 1 : 4;
-  if (t < kMaxModels) {
-    S.mvalid[t] = 0;
-    S.mtype[t] = t < 5 ? 2 : 3;
-    S.morder[t] = t < 5 ? t : 0;
-    S.mshift[t] = 0;
-    if (t < 5 && t <= fmax) S.mvalid[t] = 1;
-  }
-  // ---- 5. LPC analysis per window (3.4-3.7)
-  const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
-  const int prec = qlp_precision(bps, n);
-  if (cfg.nsub > 0 && lmax > 0) {
-    for (int wi = 0; wi < a.nwin; wi++) {
-      const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
-      __syncthreads();
-      for (int i = t; i < n + 32; i += kThreads) S.u.wf[i] = (i < n) ? (float)S.smp[i] * win[i] : 0.0f;
-      __syncthreads();
-      float wl[kChunk + kMaxLpc];
-#pragma unroll
-      for (int j = 0; j < kChunk + kMaxLpc; j++) wl[j] = S.u.wf[i0 + j];
-      // FRA-1 chunk partials: per lag, sequential over the thread's 16 samples.  The product of two
-      // floats is exact in double, so fma(a, b, acc) == acc + a*b bit for bit (oracle op order).
-      double acc[kMaxLpc + 1];
-#pragma unroll
-      for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) {
-        const double a0 = (double)wl[jj];
-#pragma unroll
-        for (int l = 0; l <= kMaxLpc; l++)
-          if (l <= lmax && i0 + jj + l < n) acc[l] = fma(a0, (double)wl[jj + l], acc[l]);
-      }
-      // pairwise tree over the 256 chunk partials: strides 1..32 in-wave, 64/128 across waves
-#pragma unroll
-      for (int l = 0; l <= kMaxLpc; l++) {
-        if (l > lmax) continue;
-        double v = acc[l];
-        for (int off = 1; off < 64; off <<= 1) {
-          double o = __shfl_down(v, off, 64);
-          v = v + o;
-        }
-        if (lane == 0) S.red[wv][l] = v;
-      }
-      __syncthreads();
-      if (t == 0) {
-        for (int l = 0; l <= lmax; l++) S.autoc[l] = (S.red[0][l] + S.red[1][l]) + (S.red[2][l] + S.red[3][l]);
-        int nord = 0;
-        if (S.autoc[0] != 0.0) nord = levinson(S.autoc, lmax, S.lp, S.err);
-        int olo = 1, ohi = nord;
-        if (wi > 0 && nord > 0) { olo = ohi = best_order_by_error(S.err, nord, n, prec + sbps); }
-        S.nord = nord; S.olo = olo; S.ohi = ohi;
-      }
-      __syncthreads();
-      const int nord = S.nord, olo = S.olo, ohi = S.ohi;
-      if (nord > 0) {
-        const int o = olo + t;
-        if (t < kMaxLpc && o <= ohi) {
-          const int m = wi == 0 ? 5 + o - 1 : 5 + kMaxLpc + wi - 1;
-          int32_t q[kMaxLpc];
-          int sh = 0;
-          bool ok = quantize(S.lp[o - 1], o, prec, q, sh);
-          S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh; S.mvalid[m] = ok ? 1 : 0;
-          for (int j = 0; j < kMaxLpc; j++) S.mcoef[m][j] = (ok && j < o) ? q[j] : 0;
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- 6. residual partition sums at the finest level P for every valid model (3.8)
-  const int P = max_porder(n, 0, cfg.max_porder);
-  const int psz = n >> P;
-  for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
-  __syncthreads();
-  for (int m = 0; m < kMaxModels; m++) {
-    if (!S.mvalid[m]) continue;  // uniform (LDS)
-    const int type = S.mtype[m], o = S.morder[m], sh = S.mshift[m];
-    int32_t q[kMaxLpc];
-#pragma unroll
-    for (int j = 0; j < kMaxLpc; j++) q[j] = S.mcoef[m][j];
-    int pidx = i0 < n ? i0 / psz : 0;
-    int pend = (pidx + 1) * psz;
-    uint64_t acc = 0;
-    bool ovf = false;
-#pragma unroll
-    for (int jj = 0; jj < kChunk; jj++) {
-      const int i = i0 + jj;
-      if (i < n && i >= o) {
-        if (i >= pend) {
-          if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
-          acc = 0;
-          pidx = i / psz;
-          pend = (pidx + 1) * psz;
-        }
-        int64_t r = model_residual<B32>(x, jj, type, o, q, sh);
-        if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
-        acc += zz64(r);
-      }
-    }
-    if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
-    if constexpr (B32) {
-      if (__any(ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
-    }
-  }
-  __syncthreads();
-
-  // ---- 7. best partition order per model (one wave per model)
-  for (int m = wv; m < kMaxModels; m += 4) {
-    if (!S.mvalid[m]) continue;
-    const int o = S.morder[m];
-    const int pm = max_porder(n, o, cfg.max_porder);
-    uint64_t Sj = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
-    for (int p = P - 1; p >= pm; p--) {
-      uint64_t a0 = shfl_u64(Sj, (2 * lane) & 63), a1 = shfl_u64(Sj, (2 * lane + 1) & 63);
-      Sj = lane < (1 << p) ? a0 + a1 : 0ull;
-    }
-    uint64_t best = 0;
-    int bp = pm;
-    for (int p = pm; p >= 0; p--) {
-      const int npp = 1 << p;
-      uint64_t bits = 0;
-      int k = 0;
-      if (lane < npp) {
-        uint64_t cnt = (uint64_t)((n >> p) - (lane == 0 ? o : 0));
-        rice_pick(cnt, Sj, k, bits);
-      }
-      const bool big = __any(lane < npp && k > 14);
-      uint64_t tot = wave_sum_u64(bits) + (uint64_t)npp * (big ? 5 : 4) + 6;
-      if (p == pm || tot <= best) { best = tot; bp = p; }
-      uint64_t a0 = shfl_u64(Sj, (2 * lane) & 63), a1 = shfl_u64(Sj, (2 * lane + 1) & 63);
-      Sj = lane < (npp >> 1) ? a0 + a1 : 0ull;
-    }
-    if (lane == 0) {
-      const bool lpc = S.mtype[m] == 3;
-      S.mest[m] = hdr + (uint64_t)o * sbps + (lpc ? 9 + (uint64_t)o * prec : 0) + best;
-      S.mporder[m] = bp;
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    int win = -1;
-    uint64_t be = 0;
-    for (int m = 0; m < kMaxModels; m++) {
-      if (!S.mvalid[m]) continue;
-      if (win < 0 || S.mest[m] < be) { be = S.mest[m]; win = m; }
-    }
-    S.winner = win;
-  }
-  __syncthreads();
-
-  // ---- 8. exact Rice bits for the winner (3.9): k per partition refined over k-1..k+1
-  const int m = S.winner;
-  const int type = S.mtype[m], o = S.morder[m], sh = S.mshift[m], ps = S.mporder[m];
-  if (wv == 0) {
-    uint64_t Sj = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
-    for (int p = P - 1; p >= ps; p--) {
-      uint64_t a0 = shfl_u64(Sj, (2 * lane) & 63), a1 = shfl_u64(Sj, (2 * lane + 1) & 63);
-      Sj = lane < (1 << p) ? a0 + a1 : 0ull;
-    }
-    if (lane < (1 << ps)) {
-      uint64_t cnt = (uint64_t)((n >> ps) - (lane == 0 ? o : 0));
-      int k;
-      uint64_t bits;
-      rice_pick(cnt, Sj, k, bits);
-      S.kpart[lane] = k;
-    }
-  }
-  __syncthreads();
-  for (int i = t; i < kMaxPart * 3; i += kThreads) (&S.u.esum[0][0])[i] = 0ull;
-  __syncthreads();
-  {
-    int32_t q[kMaxLpc];
-#pragma unroll
-    for (int j = 0; j < kMaxLpc; j++) q[j] = S.mcoef[m][j];
-    const int pz = n >> ps;
-    int pidx = i0 < n ? i0 / pz : 0, pend = (pidx + 1) * pz;
-    int k = S.kpart[pidx];
-    uint64_t e0 = 0, e1 = 0, e2 = 0;
-#pragma unroll
-    for (int jj = 0; jj < kChunk; jj++) {
-      const int i = i0 + jj;
-      if (i < n && i >= o) {
-        if (i >= pend) {
-          atomicAdd(&S.u.esum[pidx][0], (unsigned long long)e0);
-          atomicAdd(&S.u.esum[pidx][1], (unsigned long long)e1);
-          atomicAdd(&S.u.esum[pidx][2], (unsigned long long)e2);
-          e0 = e1 = e2 = 0;
-          pidx = i / pz;
-          pend = (pidx + 1) * pz;
-          k = S.kpart[pidx];
-        }
-        uint64_t u = zz64(model_residual<B32>(x, jj, type, o, q, sh));
-        e0 += k > 0 ? (u >> (k - 1)) : 0;
-        e1 += u >> k;
-        e2 += u >> (k + 1);
-      }
-    }
-    if (i0 < n) {
-      atomicAdd(&S.u.esum[pidx][0], (unsigned long long)e0);
-      atomicAdd(&S.u.esum[pidx][1], (unsigned long long)e1);
-      atomicAdd(&S.u.esum[pidx][2], (unsigned long long)e2);
-    }
-  }
-  __syncthreads();
-  if (wv == 0) {
-    const int npp = 1 << ps;
-    uint64_t best = 0;
-    int bk = 0;
-    if (lane < npp) {
-      const uint64_t cnt = (uint64_t)((n >> ps) - (lane == 0 ? o : 0));
-      const int k0 = S.kpart[lane];
-      bool first = true;
-      for (int kk = k0 - 1; kk <= k0 + 1; kk++) {
-        if (kk < 0 || kk > 30) continue;
-        uint64_t e = cnt * (uint64_t)(kk + 1) + S.u.esum[lane][kk - k0 + 1];
-        if (first || e < best) { best = e; bk = kk; first = false; }
-      }
-    }
-    const bool big = __any(lane < npp && bk > 14);
-    const uint64_t tot = wave_sum_u64(lane < npp ? best : 0ull) + (uint64_t)npp * (big ? 5 : 4) + 6;
-    const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + tot;
-    const bool verbatim = exact >= verb;
-    if (lane < npp) d->k[lane] = (uint8_t)bk;
-    if (lane < kMaxLpc) d->coef[lane] = S.mcoef[m][lane];
-    if (lane == 0) {
-      d->wasted = (uint8_t)w;
-      d->sbps = (uint8_t)sbps;
-      d->cval = 0;
-      if (verbatim) {
-        d->type = 1; d->order = 0; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
-        d->bits = (uint32_t)verb;
-      } else {
-        d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
-        d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh;
-        d->bits = (uint32_t)exact;
-      }
-    }
-  }
-}
-
-// ============================================================================ frame header
-__device__ __host__ inline int utf8_len(uint32_t v) {
-  if (v < 0x80) return 1;
-  if (v < 0x800) return 2;
-  if (v < 0x10000) return 3;
-  if (v < 0x200000) return 4;
-  if (v < 0x4000000) return 5;
-  return 6;
-}
-// writes header bytes (without CRC-8) into h, returns length
-__device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameDev& fr) {
-  int bsx, srx, srv;
-  const int bc = bs_code(fr.n, &bsx);
-  const int sc = sr_code(st.sample_rate, &srx, &srv);
-  int p = 0;
-  h[p++] = 0xFF;
-  h[p++] = 0xF8;
-  h[p++] = (uint8_t)((bc << 4) | sc);
-  h[p++] = (uint8_t)(((st.channels - 1) << 4) | (bps_code(st.bps) << 1));
-  const uint32_t v = (uint32_t)fr.index;
-  const int nb = utf8_len(v);
-  if (nb == 1) h[p++] = (uint8_t)v;
-  else {
-    h[p++] = (uint8_t)(((0xFF00u >> nb) & 0xFF) | (v >> (6 * (nb - 1))));
-    for (int i = nb - 2; i >= 0; i--) h[p++] = (uint8_t)(0x80 | ((v >> (6 * i)) & 0x3F));
-  }
-  if (bsx == 8) h[p++] = (uint8_t)(fr.n - 1);
-  else if (bsx == 16) { h[p++] = (uint8_t)((fr.n - 1) >> 8); h[p++] = (uint8_t)(fr.n - 1); }
-  if (srx == 8) h[p++] = (uint8_t)srv;
-  else if (srx == 16) { h[p++] = (uint8_t)(srv >> 8); h[p++] = (uint8_t)srv; }
-  return p;
-}
-__device__ inline int frame_header_len(const StreamDev& st, const FrameDev& fr) {
-  int bsx, srx, srv;
-  bs_code(fr.n, &bsx);
-  sr_code(st.sample_rate, &srx, &srv);
-  return 4 + utf8_len((uint32_t)fr.index) + bsx / 8 + srx / 8 + 1;  // + CRC-8
 }
 
 __global__ void k_frame_bytes(JobArgs a) {
@@ -801,8 +173,8 @@ __device__ void flush_words(PackSmem& S, int nfull, uint8_t* out, uint64_t F, in
   }
 }
 
-template <int SRC, bool B32>
-__global__ void __launch_bounds__(kThreads) k_pack(JobArgs a) {
+template <bool B32>
+__global__ void __launch_bounds__(kThreads) k_pack(JobArgs a, int src) {
   __shared__ PackSmem S;
   const int g = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const FrameDev fr = a.frames[g];
@@ -850,7 +222,11 @@ __global__ void __launch_bounds__(kThreads) k_pack(JobArgs a) {
   for (int c = 0; c < st.channels; c++) {
     if (t == 0) S.desc = a.sf[(size_t)g * a.cmax + c];
     // load + normalise channel c
-    for (int i = t; i < n; i += kThreads) S.smp[i] = fetch_sample<SRC>(a.raster, sample_elem(st, fr, c, i), np);
+    {
+      uint32_t o_ = 0;
+      int32_t a_ = 0, b_ = 0;
+      load_channel(src, a.raster, st, fr, c, np, S.smp, o_, a_, b_);
+    }
     __syncthreads();
     const SfDesc& d = S.desc;
     const int type = d.type, w = d.wasted, sbps = d.sbps, o = d.order;
@@ -898,23 +274,37 @@ __global__ void __launch_bounds__(kThreads) k_pack(JobArgs a) {
         int i = i0 - 12 + j;
         x[j] = (i >= 0 && i < n) ? S.smp[i] : 0;
       }
+      // one generic predictor body for FIXED (integer taps, shift 0) and LPC subframes
       int32_t q[kMaxLpc];
 #pragma unroll
       for (int j = 0; j < kMaxLpc; j++) q[j] = d.coef[j];
+      if (type == 2) {
+        const int32_t f[5][4] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, -1, 0, 0}, {3, -3, 1, 0}, {4, -6, 4, -1}};
+#pragma unroll
+        for (int j = 0; j < kMaxLpc; j++) q[j] = j < 4 ? f[o][j] : 0;
+      }
+      const int shv = type == 3 ? d.shift : 0;
       uint32_t u[kChunk];
       uint32_t len[kChunk];
       uint32_t tot = 0;
+      int pidx = i0 < n ? i0 / pz : 0;
+      int pend = (pidx + 1) * pz;
+      uint32_t pstartmask = 0;
+      uint32_t kk[kChunk];
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
         const int i = i0 + jj;
         u[jj] = 0;
         len[jj] = 0;
+        kk[jj] = 0;
         if (i < n && i >= o) {
-          const int pidx = i / pz;
+          if (i >= pend) { pidx++; pend += pz; }
           const int k = d.k[pidx];
-          const uint64_t uu = zz64(model_residual<B32>(x, jj, type, o, q, d.shift));
+          const uint64_t uu = zz64(gres<B32, kMaxLpc>(x, jj, q, shv));
           u[jj] = (uint32_t)uu;
+          kk[jj] = (uint32_t)k;
           const bool pstart = (pidx == 0) ? (i == o) : (i == pidx * pz);
+          if (pstart) pstartmask |= 1u << jj;
           len[jj] = (uint32_t)(uu >> k) + 1u + (uint32_t)k + (pstart ? (uint32_t)pb : 0u);
           tot += len[jj];
         }
@@ -932,13 +322,10 @@ __global__ void __launch_bounds__(kThreads) k_pack(JobArgs a) {
       uint32_t p = pos + base;
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
-        const int i = i0 + jj;
-        if (i < n && i >= o) {
-          const int pidx = i / pz;
-          const int k = d.k[pidx];
-          const bool pstart = (pidx == 0) ? (i == o) : (i == pidx * pz);
+        if (len[jj]) {
+          const int k = (int)kk[jj];
           uint32_t pp = p;
-          if (pstart) { lds_put(S.buf, pp, (uint32_t)k, pb); pp += pb; }
+          if ((pstartmask >> jj) & 1u) { lds_put(S.buf, pp, (uint32_t)k, pb); pp += pb; }
           const uint32_t qv = u[jj] >> k;
           const uint32_t code = (k == 0) ? 1u : ((1u << k) | (u[jj] & ((1u << k) - 1u)));
           lds_put(S.buf, pp + qv, code, k + 1);
@@ -1000,21 +387,6 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
   return hipGetLastError();
 }
 
-hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s) {
-  dim3 grid((unsigned)a.nframes_total, (unsigned)a.cmax);
-  switch (src) {
-#define M(S_)                                                          \
-  case S_:                                                             \
-    if (b32) k_analyze<S_, true><<<grid, kThreads, 0, s>>>(a);         \
-    else k_analyze<S_, false><<<grid, kThreads, 0, s>>>(a);            \
-    break;
-    FRA_SRC_CASES(M)
-#undef M
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
   k_frame_bytes<<<(a.nframes_total + 1 + 255) / 256, 256, 0, s>>>(a);
   return hipGetLastError();
@@ -1022,16 +394,8 @@ hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
 
 hipError_t launch_pack(int src, bool b32, const JobArgs& a, hipStream_t s) {
   dim3 grid((unsigned)a.nframes_total);
-  switch (src) {
-#define M(S_)                                                       \
-  case S_:                                                          \
-    if (b32) k_pack<S_, true><<<grid, kThreads, 0, s>>>(a);         \
-    else k_pack<S_, false><<<grid, kThreads, 0, s>>>(a);            \
-    break;
-    FRA_SRC_CASES(M)
-#undef M
-    default: return hipErrorInvalidValue;
-  }
+  if (b32) k_pack<true><<<grid, kThreads, 0, s>>>(a, src);
+  else k_pack<false><<<grid, kThreads, 0, s>>>(a, src);
   return hipGetLastError();
 }
 
