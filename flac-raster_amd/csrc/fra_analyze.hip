@@ -26,72 +26,14 @@
 
 namespace fra {
 
-// ---------------------------------------------------------------- DPP helpers (gfx9 encodings)
-enum : int { DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BC15 = 0x142, DPP_BC31 = 0x143 };
-template <int CTRL, int RM>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t old = 0) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xF, false);
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
-  const uint32_t lo = dpp32<CTRL, RM>((uint32_t)v), hi = dpp32<CTRL, RM>((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ double dppf64(double v) {
-  return __longlong_as_double((long long)dpp64<CTRL, RM>((uint64_t)__double_as_longlong(v)));
-}
-// step s of the upper-lane tree: lane j adds lane j - 2^s (the lower half of its 2^(s+1) group)
-template <int S>
-__device__ __forceinline__ uint64_t up_add64(uint64_t v) {
-  if constexpr (S == 0) return v + dpp64<DPP_SHR1, 0xF>(v);
-  else if constexpr (S == 1) return v + dpp64<DPP_SHR2, 0xF>(v);
-  else if constexpr (S == 2) return v + dpp64<DPP_SHR4, 0xF>(v);
-  else if constexpr (S == 3) return v + dpp64<DPP_SHR8, 0xF>(v);
-  else if constexpr (S == 4) return v + dpp64<DPP_BC15, 0xA>(v);
-  else return v + dpp64<DPP_BC31, 0xC>(v);
-}
-// FRA-1 autocorrelation tree over one wave's 64 chunk partials; result at lane 63
-__device__ __forceinline__ double tree64(double v) {
-  v = v + dppf64<DPP_SHR1, 0xF>(v);
-  v = v + dppf64<DPP_SHR2, 0xF>(v);
-  v = v + dppf64<DPP_SHR4, 0xF>(v);
-  v = v + dppf64<DPP_SHR8, 0xF>(v);
-  v = v + dppf64<DPP_BC15, 0xA>(v);
-  v = v + dppf64<DPP_BC31, 0xC>(v);
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {  // wave-uniform result
-  v += dpp32<DPP_SHR1, 0xF>(v);
-  v += dpp32<DPP_SHR2, 0xF>(v);
-  v += dpp32<DPP_SHR4, 0xF>(v);
-  v += dpp32<DPP_SHR8, 0xF>(v);
-  v += dpp32<DPP_BC15, 0xA>(v);
-  v += dpp32<DPP_BC31, 0xC>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ uint32_t wave_min32(uint32_t v) {  // wave-uniform result
-  v = min(v, dpp32<DPP_SHR1, 0xF>(v, ~0u));
-  v = min(v, dpp32<DPP_SHR2, 0xF>(v, ~0u));
-  v = min(v, dpp32<DPP_SHR4, 0xF>(v, ~0u));
-  v = min(v, dpp32<DPP_SHR8, 0xF>(v, ~0u));
-  v = min(v, dpp32<DPP_BC15, 0xA>(v, ~0u));
-  v = min(v, dpp32<DPP_BC31, 0xC>(v, ~0u));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
-  v |= dpp32<DPP_SHR1, 0xF>(v);
-  v |= dpp32<DPP_SHR2, 0xF>(v);
-  v |= dpp32<DPP_SHR4, 0xF>(v);
-  v |= dpp32<DPP_SHR8, 0xF>(v);
-  v |= dpp32<DPP_BC15, 0xA>(v);
-  v |= dpp32<DPP_BC31, 0xC>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
+constexpr int kBufWords = kMaxBlock + 16;  // >= (max subframe bits (< 4096*32 + 64) + 31) / 32 + 1
 
 struct AnalyzeSmem {
   int32_t smp[kMaxBlock];
-  unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
+  union {
+    unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
+    uint32_t buf[kBufWords];                        // encoded subframe (big-endian words, MSB first)
+  } u;
   double red[4][kMaxLpc + 1];
   double autoc[kMaxLpc + 1];
   double lp[kMaxLpc][kMaxLpc];
@@ -101,7 +43,10 @@ struct AnalyzeSmem {
   uint32_t mest[kMaxModels];
   uint32_t ired[4][3];
   int32_t kpart[kMaxPart];
-  int32_t nord, olo, ohi, winner;
+  int32_t kfin[kMaxPart];
+  uint32_t scan[4];
+  int32_t nord, olo, ohi, winner, ftype, fmethod;
+  uint32_t fbits;
 };
 
 // one level of the partition-order search; S = merge steps done so far (level p = P - S)
@@ -178,6 +123,12 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     if (t == 0) {
       d->type = 0; d->order = 0; d->wasted = 0; d->sbps = (uint8_t)bps; d->cval = vmin;
       d->bits = 8u + (uint32_t)bps; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
+      // blob: 8 header bits (type 0, no wasted bits) + the value in bps bits, MSB first
+      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+      const uint64_t v = (uint64_t)(uint32_t)vmin & (bps >= 32 ? 0xFFFFFFFFull : ((1ull << bps) - 1));
+      const uint64_t blob = v << (64 - 8 - bps);  // 8 zero header bits first
+      slot[0] = (uint32_t)(blob >> 32);
+      slot[1] = (uint32_t)blob;
     }
     return;
   }
@@ -276,7 +227,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   // ---- 4. residual partition sums at the finest level P for every valid model (3.8)
   const int P = max_porder(n, 0, cfg.max_porder);
   const int psz = n >> P;
-  for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.psum[0][0])[i] = 0ull;
+  for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
   __syncthreads();
   int32_t x[12 + kChunk];
 #pragma unroll
@@ -315,14 +266,14 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
         }
         acc = acc32;
       }
-      if (i0 < n && acc) atomicAdd(&S.psum[m][pidx0], (unsigned long long)acc);
+      if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
       if (i0 >= n) ovf = false;
     } else if (i0 < n) {
       int pidx = pidx0, pend = (pidx + 1) * psz;
       const int iend = min(i0 + kChunk, n);
       for (int i = max(i0, o); i < iend; i++) {
         if (i >= pend) {
-          if (acc) atomicAdd(&S.psum[m][pidx], (unsigned long long)acc);
+          if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
           acc = 0;
           pidx = i / psz;
           pend = (pidx + 1) * psz;
@@ -331,7 +282,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
         if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
         acc += zz64(r);
       }
-      if (acc) atomicAdd(&S.psum[m][pidx], (unsigned long long)acc);
+      if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
     }
     if constexpr (B32) {
       if (__any(ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
@@ -345,7 +296,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     if (!S.mvalid[m]) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
-    uint64_t Sv = lane < (1 << P) ? S.psum[m][lane] : 0ull;
+    uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
     uint64_t best = 0;
     int bp = pm;
     porder_level<0>(P, pm, n, o, lane, Sv, best, bp);
@@ -374,7 +325,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   const int m = S.winner;
   const int type = S.mtype[m], o = S.morder[m], sh = S.mshift[m], ps = S.mporder[m];
   if (wv == 0) {
-    uint64_t Sv = lane < (1 << P) ? S.psum[m][lane] : 0ull;
+    uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
     const int smax = P - ps;
     if (smax > 0) Sv = up_add64<0>(Sv);
     if (smax > 1) Sv = up_add64<1>(Sv);
@@ -392,7 +343,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     }
   }
   __syncthreads();
-  unsigned long long(*esum)[3] = reinterpret_cast<unsigned long long(*)[3]>(&S.psum[0][0]);
+  unsigned long long(*esum)[3] = reinterpret_cast<unsigned long long(*)[3]>(&S.u.psum[0][0]);
   for (int i = t; i < kMaxPart * 3; i += kThreads) (&esum[0][0])[i] = 0ull;
   __syncthreads();
   {
@@ -462,7 +413,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     const uint64_t tot = (uint64_t)wave_sum32(lane < npp ? (uint32_t)best : 0u) + (uint64_t)npp * (big ? 5 : 4) + 6;
     const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + tot;
     const bool verbatim = exact >= verb;
-    if (lane < npp) d->k[lane] = (uint8_t)bk;
+    if (lane < npp) { d->k[lane] = (uint8_t)bk; S.kfin[lane] = bk; }
     if (lane < kMaxLpc) d->coef[lane] = type == 3 ? S.mcoef[m][lane] : 0;
     if (lane == 0) {
       d->wasted = (uint8_t)w;
@@ -476,8 +427,84 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
         d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh;
         d->bits = (uint32_t)exact;
       }
+      S.ftype = verbatim ? 1 : type;
+      S.fmethod = big ? 1 : 0;
+      S.fbits = verbatim ? verb : (uint32_t)exact;
     }
   }
+  __syncthreads();
+
+  // ---- 7. encode the subframe (RFC 9639 9.2) into the LDS bit buffer and store it to its slot
+  const int ftype = S.ftype;
+  const uint32_t fbits = S.fbits;
+  const uint32_t nw = (fbits + 31) >> 5;
+  uint32_t* buf = S.u.buf;
+  for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
+  __syncthreads();
+  const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
+  if (t == 0) {
+    const int tcode = ftype == 1 ? 1 : ftype == 2 ? 8 + o : 31 + o;
+    lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
+    if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
+  }
+  if (ftype == 1) {
+    for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[i] & smask, sbps);
+  } else {
+    const int pb = S.fmethod ? 5 : 4;
+    for (int i = t; i < o; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[i] & smask, sbps);
+    uint32_t pos = hdr + (uint32_t)o * sbps;
+    if (ftype == 3) {
+      if (t == 0) {
+        lds_put(buf, pos, (uint32_t)(prec - 1), 4);
+        lds_put(buf, pos + 4, (uint32_t)sh & 31u, 5);
+      }
+      if (t < o) lds_put(buf, pos + 9 + (uint32_t)t * prec, (uint32_t)S.mcoef[m][t] & ((1u << prec) - 1u), prec);
+      pos += 9 + (uint32_t)o * prec;
+    }
+    if (t == 0) lds_put(buf, pos, ((uint32_t)S.fmethod << 4) | (uint32_t)ps, 6);
+    pos += 6;
+    int32_t q[MAXO];
+#pragma unroll
+    for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+    const int pz = n >> ps;
+    uint32_t uu[kChunk], kk[kChunk];  // zig-zag residual; Rice parameter | partition-start << 8
+    uint32_t tot = 0;
+    int pidx = i0 < n ? i0 / pz : 0, pend = (pidx + 1) * pz;
+    int kcur = S.kfin[pidx];
+#pragma unroll
+    for (int jj = 0; jj < kChunk; jj++) {
+      const int i = i0 + jj;
+      uu[jj] = 0;
+      kk[jj] = 0xFFFFu;
+      const uint32_t uv = fastframe ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh))
+                                    : (i < n ? (uint32_t)zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh)) : 0u);
+      if (i < n && i >= o) {
+        if (i >= pend) { pidx++; pend += pz; kcur = S.kfin[pidx]; }
+        const bool pstart = (pidx == 0) ? (i == o) : (i == pidx * pz);
+        uu[jj] = uv;
+        kk[jj] = (uint32_t)kcur | (pstart ? 0x100u : 0u);
+        tot += (uv >> kcur) + 1u + (uint32_t)kcur + (pstart ? (uint32_t)pb : 0u);
+      }
+    }
+    const uint32_t inc = wave_incl_scan32(tot);
+    if (lane == 63) S.scan[wv] = inc;
+    __syncthreads();
+    uint32_t p = pos + inc - tot;
+    for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
+#pragma unroll
+    for (int jj = 0; jj < kChunk; jj++) {
+      if (kk[jj] != 0xFFFFu) {
+        const int k = (int)(kk[jj] & 0xFF);
+        if (kk[jj] & 0x100u) { lds_put(buf, p, (uint32_t)k, pb); p += pb; }
+        const uint32_t qv = uu[jj] >> k;
+        lds_put(buf, p + qv, (k == 0) ? 1u : ((1u << k) | (uu[jj] & ((1u << k) - 1u))), k + 1);
+        p += qv + 1u + (uint32_t)k;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+  for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
 }
 
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s) {

@@ -30,7 +30,7 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
-hipError_t launch_pack(int src, bool b32, const JobArgs& a, hipStream_t s);
+hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int bands, int H, int W, void* out, hipStream_t s);
 }  // namespace fra
 
@@ -84,6 +84,9 @@ struct fra_plan {
   size_t out_cap = 0;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
+  uint16_t* d_crctab = nullptr;
+  uint32_t* d_tmp = nullptr;
+  int64_t tmp_stride = 0;
   JobArgs args{};
   // timing
   bool timing = false;
@@ -133,6 +136,40 @@ static void window_set(float* w, int N, int stride, int nsub) {
       for (int i = 0; i < N; i++) o[i] = 0.0f;
       if (b - a > 0) tukey(o + a, b - a, 0.5);
     }
+}
+
+// CRC-16 (poly x^16+x^15+x^2+1) tables for k_crc16: slice-by-4 byte tables T[k][v] = CRC of v
+// followed by k zero bytes, and M[i][0|1][b] = b * x^(8*2^i) (resp. b*x^8*x^(8*2^i)) mod P.
+static uint32_t gf16_mul(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 15; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x10000u) r ^= 0x18005u;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r & 0xFFFFu;
+}
+static std::vector<uint16_t> crc16_tables() {
+  std::vector<uint16_t> tab(1024 + 24 * 512);
+  for (int v = 0; v < 256; v++) {
+    uint32_t d = (uint32_t)v << 8;
+    for (int b = 0; b < 8; b++) d = (d & 0x8000u) ? ((d << 1) ^ 0x8005u) : (d << 1);
+    tab[v] = (uint16_t)d;
+  }
+  for (int k = 1; k < 4; k++)
+    for (int v = 0; v < 256; v++) {
+      const uint32_t p = tab[(k - 1) * 256 + v];
+      tab[k * 256 + v] = (uint16_t)(((p << 8) & 0xFFFFu) ^ tab[p >> 8]);
+    }
+  uint32_t X = 0x100;  // x^8
+  for (int i = 0; i < 24; i++) {
+    for (int b = 0; b < 256; b++) {
+      tab[1024 + i * 512 + b] = (uint16_t)gf16_mul((uint32_t)b, X);
+      tab[1024 + i * 512 + 256 + b] = (uint16_t)gf16_mul(gf16_mul((uint32_t)b, 0x100), X);
+    }
+    X = gf16_mul(X, X);
+  }
+  return tab;
 }
 
 static const char kVendor[] = "flac-raster-amd 0.1.0 gfx950 HIP";  // 32 bytes, as libFLAC's vendor string
@@ -185,6 +222,8 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_foff);
   (void)hipFree(p->d_out);
   (void)hipFree(p->d_scan_tmp);
+  (void)hipFree(p->d_crctab);
+  (void)hipFree(p->d_tmp);
   for (auto& e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;
@@ -278,6 +317,14 @@ static int plan_build(fra_plan* p) {
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, p->scan_tmp_bytes, p->d_fbytes, p->d_foff, nfr + 1,
                                           p->ctx->stream));
   HIPCHK(hipMalloc(&p->d_scan_tmp, std::max<size_t>(16, p->scan_tmp_bytes)));
+  // per-subframe slots for the encoded subframes (k_analyze -> k_assemble)
+  p->tmp_stride = ((int64_t)j.blocksize * bps + 64 + 31) / 32 + 4;
+  HIPCHK(hipMalloc(&p->d_tmp, sizeof(uint32_t) * (size_t)p->tmp_stride * std::max(1, nfr) * p->cmax));
+  {
+    const std::vector<uint16_t> ct = crc16_tables();
+    HIPCHK(hipMalloc(&p->d_crctab, sizeof(uint16_t) * ct.size()));
+    HIPCHK(hipMemcpy(p->d_crctab, ct.data(), sizeof(uint16_t) * ct.size(), hipMemcpyHostToDevice));
+  }
   JobArgs& a = p->args;
   a.streams = p->d_streams;
   a.frames = p->d_frames;
@@ -287,6 +334,9 @@ static int plan_build(fra_plan* p) {
   a.frame_bytes = p->d_fbytes;
   a.frame_off = p->d_foff;
   a.out = p->d_out;
+  a.crctab = p->d_crctab;
+  a.tmp = p->d_tmp;
+  a.tmp_stride = p->tmp_stride;
   a.nframes_total = nfr;
   a.cmax = p->cmax;
   a.blocksize = j.blocksize;
@@ -378,7 +428,7 @@ int fra_plan_execute(fra_plan* p) {
   size_t tb = p->scan_tmp_bytes;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(p->d_scan_tmp, tb, p->d_fbytes, p->d_foff, a.nframes_total + 1, s));
   if (p->timing) HIPCHK(hipEventRecord(p->ev[3], s));
-  if (a.nframes_total > 0) HIPCHK(launch_pack(p->src, p->b32, a, s));
+  HIPCHK(launch_assemble(a, s));
   if (p->timing) {
     HIPCHK(hipEventRecord(p->ev[4], s));
     p->pending_times = true;

@@ -171,6 +171,80 @@ __device__ __forceinline__ void load_channel(int src, const void* base, const St
   }
 }
 
+// ---------------------------------------------------------------- DPP helpers (gfx9 encodings)
+enum : int { DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BC15 = 0x142, DPP_BC31 = 0x143 };
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t old = 0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = dpp32<CTRL, RM>((uint32_t)v), hi = dpp32<CTRL, RM>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dppf64(double v) {
+  return __longlong_as_double((long long)dpp64<CTRL, RM>((uint64_t)__double_as_longlong(v)));
+}
+// step s of the upper-lane tree: lane j adds lane j - 2^s (the lower half of its 2^(s+1) group)
+template <int S>
+__device__ __forceinline__ uint64_t up_add64(uint64_t v) {
+  if constexpr (S == 0) return v + dpp64<DPP_SHR1, 0xF>(v);
+  else if constexpr (S == 1) return v + dpp64<DPP_SHR2, 0xF>(v);
+  else if constexpr (S == 2) return v + dpp64<DPP_SHR4, 0xF>(v);
+  else if constexpr (S == 3) return v + dpp64<DPP_SHR8, 0xF>(v);
+  else if constexpr (S == 4) return v + dpp64<DPP_BC15, 0xA>(v);
+  else return v + dpp64<DPP_BC31, 0xC>(v);
+}
+// FRA-1 autocorrelation tree over one wave's 64 chunk partials; result at lane 63
+__device__ __forceinline__ double tree64(double v) {
+  v = v + dppf64<DPP_SHR1, 0xF>(v);
+  v = v + dppf64<DPP_SHR2, 0xF>(v);
+  v = v + dppf64<DPP_SHR4, 0xF>(v);
+  v = v + dppf64<DPP_SHR8, 0xF>(v);
+  v = v + dppf64<DPP_BC15, 0xA>(v);
+  v = v + dppf64<DPP_BC31, 0xC>(v);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {  // wave-uniform result
+  v += dpp32<DPP_SHR1, 0xF>(v);
+  v += dpp32<DPP_SHR2, 0xF>(v);
+  v += dpp32<DPP_SHR4, 0xF>(v);
+  v += dpp32<DPP_SHR8, 0xF>(v);
+  v += dpp32<DPP_BC15, 0xA>(v);
+  v += dpp32<DPP_BC31, 0xC>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_min32(uint32_t v) {  // wave-uniform result
+  v = min(v, dpp32<DPP_SHR1, 0xF>(v, ~0u));
+  v = min(v, dpp32<DPP_SHR2, 0xF>(v, ~0u));
+  v = min(v, dpp32<DPP_SHR4, 0xF>(v, ~0u));
+  v = min(v, dpp32<DPP_SHR8, 0xF>(v, ~0u));
+  v = min(v, dpp32<DPP_BC15, 0xA>(v, ~0u));
+  v = min(v, dpp32<DPP_BC31, 0xC>(v, ~0u));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  v |= dpp32<DPP_SHR1, 0xF>(v);
+  v |= dpp32<DPP_SHR2, 0xF>(v);
+  v |= dpp32<DPP_SHR4, 0xF>(v);
+  v |= dpp32<DPP_SHR8, 0xF>(v);
+  v |= dpp32<DPP_BC15, 0xA>(v);
+  v |= dpp32<DPP_BC31, 0xC>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// inclusive prefix sum over the wave (Hillis-Steele inside rows, then row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += dpp32<DPP_SHR1, 0xF>(v);
+  v += dpp32<DPP_SHR2, 0xF>(v);
+  v += dpp32<DPP_SHR4, 0xF>(v);
+  v += dpp32<DPP_SHR8, 0xF>(v);
+  v += dpp32<DPP_BC15, 0xA>(v);
+  v += dpp32<DPP_BC31, 0xC>(v);
+  return v;
+}
+
 // ---------------------------------------------------------------- integer helpers
 __device__ __forceinline__ uint64_t zz64(int64_t r) {
   return r >= 0 ? ((uint64_t)r << 1) : ((((uint64_t)(-(r + 1))) << 1) | 1u);
@@ -417,6 +491,19 @@ __device__ __forceinline__ int64_t gres_lds(const int32_t* smp, int i, const int
     int32_t sum = 0;
     for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], smp[max(0, i - 1 - j)]);
     return (int64_t)(smp[i] - (sum >> sh));
+  }
+}
+
+// OR a value of `width` bits (1..32, already masked) at bit position pos of a big-endian word buffer
+__device__ __forceinline__ void lds_put(uint32_t* buf, uint32_t pos, uint32_t v, int width) {
+  // v already masked to width (1..32); MSB-first bit order within big-endian words
+  const uint32_t w0 = pos >> 5, off = pos & 31;
+  const int end = (int)off + width;
+  if (end <= 32) {
+    atomicOr(&buf[w0], v << (32 - end));
+  } else {
+    atomicOr(&buf[w0], v >> (end - 32));
+    atomicOr(&buf[w0 + 1], v << (64 - end));
   }
 }
 

@@ -169,6 +169,9 @@ struct JobArgs {
   unsigned long long* frame_bytes;  // [nframes_total + 1] (last = 0)
   unsigned long long* frame_off;  // [nframes_total + 1] exclusive scan of frame_bytes
   uint8_t* out;            // concatenated frames
+  const uint16_t* crctab;  // CRC-16 slice-by-4 tables [4][256] + multiply-by-x^(8*2^i) tables [24][2][256]
+  uint32_t* tmp;           // encoded subframes: slot (frame*cmax + channel) of tmp_stride words
+  int64_t tmp_stride;
   int32_t nframes_total;
   int32_t cmax;
   int32_t blocksize;

@@ -1,0 +1,153 @@
+// fra_pack.hip -- k_assemble: frame assembly + CRC-16 (one workgroup per frame).
+//
+// Emits what libFLAC's frame writer emits for every 4,096-sample block that
+// FLAC__stream_encoder_process_interleaved / _finish produce under the pyflac calls at
+// src/flac_raster/converter.py:153-154 and src/flac_raster/spatial_encoder.py:303-304:
+// frame header (RFC 9639 9.1, CRC-8) ++ subframes (9.2, encoded by k_analyze into per-subframe
+// slots) ++ zero pad to a byte ++ CRC-16.
+//
+// Gather formulation: every thread builds whole output dwords.  Global dword G0+k (G0 = F>>2)
+// holds frame bits [8(4k-A), +32) (A = F & 3): the header and the channel blobs are laid end to end
+// at known bit offsets, so each 32-bit window is a funnel-shifted read from at most a few segments.
+// Dwords entirely inside the frame are written with one aligned store; the first/last dwords
+// (shared with the neighbouring frames) get byte stores.
+//
+// CRC-16 (poly x^16+x^15+x^2+1, init 0) on the same dwords, no extra pass: thread t folds the dwords
+// with virtual index v = k + pad == t (mod 256) by Horner (acc = acc * x^(32*256) ^ crc4(dword)); the
+// front pad (and the A bytes before F, which read as zero) are leading zeros, which leave a
+// zero-initialised CRC unchanged.  The 256 accumulators are combined by a DPP upper-lane tree
+// (x^(32*2^l) multipliers, host-precomputed byte tables), then the < 4 tail bytes byte-wise.
+#include "fra_device.h"
+
+namespace fra {
+
+// multiply a CRC-16 remainder by x^(8*2^i) mod P: two byte-table lookups
+__device__ __forceinline__ uint32_t crc_mul(const uint16_t* M, int i, uint32_t c) {
+  const uint16_t* m = M + (size_t)i * 512;
+  return (uint32_t)m[c & 0xFF] ^ (uint32_t)m[256 + (c >> 8)];
+}
+
+struct AssembleSmem {
+  uint16_t T[4][256];   // slice-by-4: T[k][v] = CRC of v followed by k zero bytes
+  uint16_t MH[2][256];  // multiply by x^(32*256) (Horner step)
+  uint32_t hdrw[8];     // frame header (+CRC-8) as big-endian words
+  uint32_t seg[8 + 2];  // seg[0] = 0, seg[1] = header bits, seg[c+2] = end of channel c
+  uint32_t crcw[4];
+};
+
+// `take` (1..32) bits at bit b of a big-endian word array, right-aligned
+__device__ __forceinline__ uint32_t bits_at(const uint32_t* w, uint32_t b, int take) {
+  const uint64_t X = ((uint64_t)w[b >> 5] << 32) | w[(b >> 5) + 1];
+  return (uint32_t)((X << (b & 31)) >> (64 - take));
+}
+
+__global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
+  __shared__ AssembleSmem S;
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int i = t; i < 1024; i += kThreads) (&S.T[0][0])[i] = a.crctab[i];
+  const uint16_t* M = a.crctab + 1024;
+  for (int i = t; i < 512; i += kThreads) (&S.MH[0][0])[i] = M[10 * 512 + i];  // x^(8*2^10) = x^(32*256)
+  const FrameDev fr = a.frames[g];
+  const StreamDev st = a.streams[fr.stream];
+  const int C = st.channels;
+  if (t == 0) {
+    uint8_t h[24];
+    int hl = frame_header(h, st, fr);
+    uint32_t c8 = 0;
+    for (int i = 0; i < hl; i++) {
+      c8 ^= h[i];
+      for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) : (c8 << 1);
+      c8 &= 0xFF;
+    }
+    h[hl++] = (uint8_t)c8;
+    for (int j = 0; j < 8; j++) S.hdrw[j] = 0;
+    for (int b = 0; b < hl; b++) S.hdrw[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
+    S.seg[0] = 0;
+    S.seg[1] = (uint32_t)hl * 8;
+    for (int c = 0; c < C; c++) S.seg[c + 2] = S.seg[c + 1] + a.sf[(size_t)g * a.cmax + c].bits;
+  }
+  __syncthreads();
+  const uint32_t TB = S.seg[C + 1];             // frame bits before the byte pad
+  const uint64_t F = a.frame_off[g];
+  const uint64_t L = a.frame_bytes[g] - 2;      // = ceil(TB / 8): bytes covered by the CRC-16
+  const uint32_t A = (uint32_t)(F & 3);
+  uint32_t* gw = (uint32_t*)(a.out + (F - A));  // dword k of this frame's span
+  const int64_t ND = (int64_t)((F + L - 1) >> 2) - (int64_t)(F >> 2) + 1;  // dwords touching the frame
+  const int64_t NF = (int64_t)((F + L) >> 2) - (int64_t)(F >> 2);          // dwords ending inside it
+  const int pad = (int)((kThreads - (NF % kThreads)) % kThreads);
+  const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
+
+  // 32 frame bits starting at (possibly negative) bit position bp; bits outside [0, TB) read 0
+  auto window = [&](int64_t bp) -> uint32_t {
+    uint32_t res = 0;
+    int filled = 0;
+    if (bp < 0) {
+      filled = (int)min<int64_t>(32, -bp);
+      bp = 0;
+    }
+    int s = 0;
+    while (filled < 32 && bp < (int64_t)TB) {
+      while ((int64_t)S.seg[s + 1] <= bp) s++;
+      const uint32_t take = (uint32_t)min<int64_t>(32 - filled, (int64_t)S.seg[s + 1] - bp);
+      const uint32_t rel = (uint32_t)(bp - S.seg[s]);
+      const uint32_t v =
+          s == 0 ? bits_at(S.hdrw, rel, (int)take) : bits_at(slots + (size_t)(s - 1) * a.tmp_stride, rel, (int)take);
+      res |= take == 32 ? v : (v << (32 - filled - (int)take));
+      filled += (int)take;
+      bp += take;
+    }
+    return res;
+  };
+
+  uint32_t acc = 0;
+  int64_t k = (int64_t)t - pad;
+  if (k < 0) k += kThreads;
+  for (; k < ND; k += kThreads) {
+    const uint32_t val = window(8 * (4 * k - (int64_t)A));
+    if ((k > 0 || A == 0) && k < NF) {
+      gw[k] = __builtin_bswap32(val);
+    } else {
+      for (int b = 0; b < 4; b++) {
+        const int64_t fb = 4 * k - (int64_t)A + b;  // frame byte index
+        if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val >> (24 - 8 * b));
+      }
+    }
+    if (k < NF) {
+      const uint32_t c4 = (uint32_t)S.T[3][val >> 24] ^ (uint32_t)S.T[2][(val >> 16) & 0xFF] ^
+                          (uint32_t)S.T[1][(val >> 8) & 0xFF] ^ (uint32_t)S.T[0][val & 0xFF];
+      acc = ((uint32_t)S.MH[0][acc & 0xFF] ^ (uint32_t)S.MH[1][acc >> 8]) ^ c4;
+    }
+  }
+  // combine: lane order == virtual dword order; left groups are multiplied by x^(32*2^l)
+  acc ^= crc_mul(M, 2, dpp32<DPP_SHR1, 0xF>(acc));
+  acc ^= crc_mul(M, 3, dpp32<DPP_SHR2, 0xF>(acc));
+  acc ^= crc_mul(M, 4, dpp32<DPP_SHR4, 0xF>(acc));
+  acc ^= crc_mul(M, 5, dpp32<DPP_SHR8, 0xF>(acc));
+  acc ^= crc_mul(M, 6, dpp32<DPP_BC15, 0xA>(acc));
+  acc ^= crc_mul(M, 7, dpp32<DPP_BC31, 0xC>(acc));
+  if (lane == 63) S.crcw[wv] = acc;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t c01 = crc_mul(M, 8, S.crcw[0]) ^ S.crcw[1];
+    const uint32_t c23 = crc_mul(M, 8, S.crcw[2]) ^ S.crcw[3];
+    uint32_t crc = crc_mul(M, 9, c01) ^ c23;
+    // tail: frame bytes [4*NF - A, L) not covered by whole dwords
+    const int64_t tb0 = 4 * NF - (int64_t)A;
+    if (tb0 < (int64_t)L) {
+      const uint32_t val = window(8 * tb0);
+      for (int64_t fb = tb0; fb < (int64_t)L; fb++) {
+        const uint32_t by = (val >> (24 - 8 * (int)(fb - tb0))) & 0xFF;
+        crc = ((crc << 8) ^ S.T[0][((crc >> 8) ^ by) & 0xFF]) & 0xFFFF;
+      }
+    }
+    a.out[F + L] = (uint8_t)(crc >> 8);
+    a.out[F + L + 1] = (uint8_t)crc;
+  }
+}
+
+hipError_t launch_assemble(const JobArgs& a, hipStream_t s) {
+  if (a.nframes_total > 0) k_assemble<<<(unsigned)a.nframes_total, kThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace fra
