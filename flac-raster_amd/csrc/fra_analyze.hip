@@ -22,18 +22,24 @@
 //      sums, Rice estimate per partition leader, per-order totals by DPP wave sums
 //   6. winner = first minimal estimate (DPP argmin); exact Rice bits for the winner with k refined
 //      over k-1..k+1; VERBATIM if not smaller
+#include <type_traits>
+
 #include "fra_device.h"
 
 namespace fra {
 
-constexpr int kBufWords = kMaxBlock + 16;  // >= (max subframe bits (< 4096*32 + 64) + 31) / 32 + 1
+// encoded-subframe buffer: >= (max subframe bits + 31) / 32 + 1 words (VERBATIM bound)
+template <bool B32>
+constexpr int buf_words() { return B32 ? kMaxBlock + 16 : kMaxBlock / 2 + 16; }
 
+template <bool B32>
 struct AnalyzeSmem {
   int32_t smp[kMaxBlock];
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
-    uint32_t buf[kBufWords];                        // encoded subframe (big-endian words, MSB first)
+    uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
   } u;
+  unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
   double red[4][kMaxLpc + 1];
   double autoc[kMaxLpc + 1];
   double lp[kMaxLpc][kMaxLpc];
@@ -49,36 +55,127 @@ struct AnalyzeSmem {
   uint32_t fbits;
 };
 
-// one level of the partition-order search; S = merge steps done so far (level p = P - S)
-template <int S>
-__device__ __forceinline__ void porder_level(int P, int pm, int n, int o, int lane, uint64_t& Sv, uint64_t& best,
-                                             int& bp) {
-  if (S > P) return;
-  const int p = P - S;
-  if (p <= pm) {  // wave-uniform
-    uint32_t bits32 = 0;
-    bool big = false;
-    if (lane < (1 << P) && ((lane + 1) & ((1 << S) - 1)) == 0) {  // upper lane of its group = leader
-      const int j = lane >> S;
-      const uint64_t cnt = (uint64_t)((n >> p) - (j == 0 ? o : 0));
-      int k;
-      uint64_t bits;
-      rice_pick(cnt, Sv, k, bits);
-      bits32 = (uint32_t)bits;
-      big = k > 14;
+// ---- fast-path residual sums over the thread's 16 samples (one finest partition per thread);
+// ---- samples jj < skip (warm-up: thread 0 only) are masked
+template <bool B32>
+__device__ __forceinline__ void acc_zz(int64_t r, bool on, uint64_t& acc, bool& ovf) {
+  if constexpr (B32) {
+    ovf |= on && (r > INT32_MAX || r < INT32_MIN);
+    acc += on ? zz64(r) : 0ull;
+  } else {
+    acc += on ? zz32((int32_t)r) : 0u;  // |r| < 2^27: 16 values fit in 32 bits, widened once
+  }
+}
+// FIXED orders 0..4 at once: the order-k residual is the k-th finite difference of the samples,
+// the same integers as the oracle's closed forms (s, s-s1, s-2s1+s2, ...)
+template <bool B32>
+__device__ __forceinline__ void fixed_sums_fast(const int32_t* x, int i0, uint64_t (&acc)[5], bool (&ovf)[5]) {
+  using T = typename std::conditional<B32, int64_t, int32_t>::type;
+  T d[kChunk + 4];  // d[j] = current difference at x index j + 8
+#pragma unroll
+  for (int j = 0; j < kChunk + 4; j++) d[j] = (T)x[8 + j];
+#pragma unroll
+  for (int k = 0; k <= 4; k++) {
+    if (k > 0) {
+#pragma unroll
+      for (int j = kChunk + 3; j >= k; j--) d[j] = d[j] - d[j - 1];
     }
-    const uint64_t tot = (uint64_t)wave_sum32(bits32) + (uint64_t)(1 << p) * (__any(big) ? 5 : 4) + 6;
-    if (p == pm || tot <= best) { best = tot; bp = p; }
+    const int skip = k > i0 ? k - i0 : 0;
+    uint64_t s = 0;
+    bool o = false;
+#pragma unroll
+    for (int jj = 0; jj < kChunk; jj++) acc_zz<B32>((int64_t)d[jj + 4], jj >= skip, s, o);
+    acc[k] = s;
+    ovf[k] = o;
   }
-  if constexpr (S < 6) {
-    if (S < P) Sv = up_add64<S>(Sv);
+}
+template <bool B32, int O>
+__device__ __forceinline__ uint64_t lpc_sum_fast(const int32_t* x, const int32_t* q, int sh, int skip, bool& ovf) {
+  uint64_t acc = 0;
+#pragma unroll
+  for (int jj = 0; jj < kChunk; jj++) acc_zz<B32>(gres<B32, O>(x, jj, q, sh), jj >= skip, acc, ovf);
+  return acc;
+}
+
+// Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at
+// lane 2^p + j (level P = 6 nodes in a second register), so each lane runs ONE Rice estimate and
+// the per-level totals come out of a single upper-lane DPP chain (level p's segment is the aligned
+// lane group [2^p, 2^(p+1)), summed after p steps) and one ballot.  Same totals and tie rule as the
+// oracle's per-level loop (iterate p = pm..0, keep '<=').
+__device__ __forceinline__ void porder_search(const unsigned long long* psum, unsigned long long* node, int P, int pm,
+                                              int n, int o, int lane, uint64_t& best_out, int& bp_out) {
+  // node sums: finest sums S_j, then upper-lane group sums (leader lane of 2^s lanes = (j+1)2^s - 1)
+  uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
+  if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
+#define FRA_NODE_STEP(S_)                                                          \
+  if (P > S_) {                                                                    \
+    Sv = up_add64<S_>(Sv);                                                         \
+    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
+      node[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = Sv;                         \
   }
+  FRA_NODE_STEP(0)
+  FRA_NODE_STEP(1)
+  FRA_NODE_STEP(2)
+  FRA_NODE_STEP(3)
+  FRA_NODE_STEP(4)
+  FRA_NODE_STEP(5)
+#undef FRA_NODE_STEP
+  // this wave's node stores -> its own reads (DS ops of one wave complete in order)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  // levels 0..min(P,5): lane = 2^p + j
+  uint32_t bits32 = 0;
+  bool big = false;
+  const int p = lane ? 31 - __clz(lane) : 0;
+  if (lane >= 1 && p <= P && p <= pm) {
+    const int j = lane - (1 << p);
+    const uint64_t cnt = (uint64_t)((n >> p) - (j == 0 ? o : 0));
+    int k;
+    uint64_t bits;
+    rice_pick(cnt, node[lane], k, bits);
+    bits32 = (uint32_t)bits;
+    big = k > 14;
+  }
+  const uint64_t bigm = __ballot(big);
+  uint32_t tot[7];
+  uint32_t v = bits32;
+  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
+  v += dpp32<DPP_SHR1, 0xF>(v);
+  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+  v += dpp32<DPP_SHR2, 0xF>(v);
+  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
+  v += dpp32<DPP_SHR4, 0xF>(v);
+  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  v += dpp32<DPP_SHR8, 0xF>(v);
+  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  v += dpp32<DPP_BC15, 0xA>(v);
+  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  tot[6] = 0;
+  bool big6 = false;
+  if (P == 6 && pm == 6) {  // level 6: 64 nodes at node[64 + lane]
+    const uint64_t cnt = (uint64_t)((n >> 6) - (lane == 0 ? o : 0));
+    int k;
+    uint64_t bits;
+    rice_pick(cnt, node[64 + lane], k, bits);
+    tot[6] = wave_sum32((uint32_t)bits);
+    big6 = __any(k > 14);
+  }
+  uint64_t best = 0;
+  int bp = pm;
+  for (int q = pm; q >= 0; q--) {
+    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
+    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
+    if (q == pm || t <= best) { best = t; bp = q; }
+  }
+  best_out = best;
+  bp_out = bp;
 }
 
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
-  __shared__ AnalyzeSmem S;
+  __shared__ AnalyzeSmem<B32> S;
   const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
@@ -238,54 +335,83 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? kMaxLpc + a.nwin - 1 : 0);
-  for (int m = 0; m < nmod; m++) {
-    if (!S.mvalid[m]) continue;  // wave-uniform (LDS)
-    const int o = S.morder[m];
-    const int sh = __builtin_amdgcn_readfirstlane(S.mshift[m]);
-    int32_t q[MAXO];
+  if (fastframe) {
+    if constexpr (!B32) {
+      // FIXED 0..4 by finite differences (every fixed model is valid here: n >= 16)
+      uint64_t facc[5];
+      bool fovf[5];
+      fixed_sums_fast<false>(x, i0, facc, fovf);
 #pragma unroll
-    for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
-    bool ovf = false;
-    uint64_t acc = 0;
-    if (fastframe) {
-      const int skip = o > i0 ? o - i0 : 0;  // warm-up samples (thread 0 only) are masked
-      if constexpr (B32) {
+      for (int k = 0; k <= 4; k++)
+        if (i0 < n && facc[k]) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)facc[k]);
+    } else {
+      // 32-bps: FIXED k as the 4-tap integer predictor (int64), one model at a time
+      for (int m = 0; m < 5; m++) {
+        const int o = m;
+        int32_t q[4];
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) {
-          const int64_t r = gres<B32, MAXO>(x, jj, q, sh);
-          const bool on = jj >= skip;
-          ovf |= on && (r > INT32_MAX || r < INT32_MIN);
-          acc += on ? zz64(r) : 0ull;
-        }
-      } else {
-        uint32_t acc32 = 0;  // |r| < 2^27 on the 16-bit path: 16 zig-zag values fit in 32 bits
+        for (int j = 0; j < 4; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+        const int skip = o > i0 ? o - i0 : 0;
+        bool ovf = false;
+        const uint64_t acc = lpc_sum_fast<true, 4>(x, q, 0, skip, ovf);
+        if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
+        if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;
+      }
+    }
+    // LPC orders: exact-order tap bodies
+    for (int m = 5; m < nmod; m++) {
+      if (!S.mvalid[m]) continue;  // wave-uniform (LDS)
+      const int o = S.morder[m];
+      const int sh = __builtin_amdgcn_readfirstlane(S.mshift[m]);
+      int32_t q[MAXO];
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) {
-          const int32_t r = (int32_t)gres<B32, MAXO>(x, jj, q, sh);
-          acc32 += jj >= skip ? zz32(r) : 0u;
-        }
-        acc = acc32;
+      for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+      const int skip = o > i0 ? o - i0 : 0;
+      bool ovf = false;
+      uint64_t acc = 0;
+      switch (o) {
+#define FRA_CASE(O_) \
+  case O_:           \
+    if constexpr (O_ <= MAXO) acc = lpc_sum_fast<B32, O_>(x, q, sh, skip, ovf); \
+    break;
+        FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6)
+        FRA_CASE(7) FRA_CASE(8) FRA_CASE(9) FRA_CASE(10) FRA_CASE(11) FRA_CASE(12)
+#undef FRA_CASE
       }
       if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
-      if (i0 >= n) ovf = false;
-    } else if (i0 < n) {
-      int pidx = pidx0, pend = (pidx + 1) * psz;
-      const int iend = min(i0 + kChunk, n);
-      for (int i = max(i0, o); i < iend; i++) {
-        if (i >= pend) {
-          if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
-          acc = 0;
-          pidx = i / psz;
-          pend = (pidx + 1) * psz;
-        }
-        const int64_t r = gres_lds<B32, MAXO>(S.smp, i, q, sh);
-        if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
-        acc += zz64(r);
+      if constexpr (B32) {
+        if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
       }
-      if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
     }
-    if constexpr (B32) {
-      if (__any(ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
+  } else {
+    for (int m = 0; m < nmod; m++) {
+      if (!S.mvalid[m]) continue;  // wave-uniform (LDS)
+      const int o = S.morder[m];
+      const int sh = __builtin_amdgcn_readfirstlane(S.mshift[m]);
+      int32_t q[MAXO];
+#pragma unroll
+      for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+      bool ovf = false;
+      uint64_t acc = 0;
+      if (i0 < n) {
+        int pidx = pidx0, pend = (pidx + 1) * psz;
+        const int iend = min(i0 + kChunk, n);
+        for (int i = max(i0, o); i < iend; i++) {
+          if (i >= pend) {
+            if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
+            acc = 0;
+            pidx = i / psz;
+            pend = (pidx + 1) * psz;
+          }
+          const int64_t r = gres_lds<B32, MAXO>(S.smp, i, q, sh);
+          if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
+          acc += zz64(r);
+        }
+        if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
+      }
+      if constexpr (B32) {
+        if (__any(ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
+      }
     }
   }
   __syncthreads();
@@ -296,16 +422,9 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     if (!S.mvalid[m]) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
-    uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
     uint64_t best = 0;
     int bp = pm;
-    porder_level<0>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<1>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<2>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<3>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<4>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<5>(P, pm, n, o, lane, Sv, best, bp);
-    porder_level<6>(P, pm, n, o, lane, Sv, best, bp);
+    porder_search(S.u.psum[m], S.node[wv], P, pm, n, o, lane, best, bp);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
