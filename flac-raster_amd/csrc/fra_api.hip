@@ -32,6 +32,8 @@ hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int bands, int H, int W, void* out, hipStream_t s);
+hipError_t launch_normalize_flat(int src, const void* data, uint64_t n, int bps, NormDev* nd, int has_min, double omin,
+                                 int has_max, double omax, void* out, hipStream_t s);
 }  // namespace fra
 
 using namespace fra;
@@ -175,6 +177,16 @@ static std::vector<uint16_t> crc16_tables() {
 static const char kVendor[] = "flac-raster-amd 0.1.0 gfx950 HIP";  // 32 bytes, as libFLAC's vendor string
 
 extern "C" {
+
+int fra_internal_set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
 
 const char* fra_last_error(void) { return g_err.c_str(); }
 int fra_abi_version(void) { return FRA_ABI_VERSION; }
@@ -399,7 +411,7 @@ int fra_plan_create(fra_ctx* ctx, const fra_job* job, fra_plan** out) {
 
 static void collect_times(fra_plan* p) {
   if (!p->pending_times) return;
-  hipEventSynchronize(p->ev[4]);
+  (void)hipEventSynchronize(p->ev[4]);
   for (int k = 0; k < 4; k++) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, p->ev[k], p->ev[k + 1]) == hipSuccess) p->ms[k] += ms;
@@ -449,6 +461,7 @@ int fra_plan_result(fra_plan* p, fra_stream_info* infos, uint64_t* total) {
   if (!p) return set_err(FRA_E_INVALID, "null plan");
   if (!p->executed) return set_err(FRA_E_STATE, "plan not executed");
   (void)hipSetDevice(p->ctx->device);
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));
   const int nfr = p->args.nframes_total;
   std::vector<unsigned long long> off(nfr + 1);
   HIPCHK(hipMemcpy(off.data(), p->d_foff, sizeof(unsigned long long) * (nfr + 1), hipMemcpyDeviceToHost));
@@ -481,6 +494,19 @@ int fra_plan_download(fra_plan* p, uint8_t* host_out, uint64_t capacity) {
   if (capacity < total) return set_err(FRA_E_INVALID, "capacity %llu < %llu", (unsigned long long)capacity,
                                        (unsigned long long)total);
   if (total) HIPCHK(hipMemcpy(host_out, p->d_out, total, hipMemcpyDeviceToHost));
+  return FRA_OK;
+}
+
+int fra_plan_frame_offsets(fra_plan* p, uint64_t* offsets, uint64_t n) {
+  if (!p || !offsets) return set_err(FRA_E_INVALID, "null argument");
+  if (!p->executed) return set_err(FRA_E_STATE, "plan not executed");
+  const uint64_t nfr = (uint64_t)p->args.nframes_total;
+  if (n != nfr + 1) return set_err(FRA_E_INVALID, "frame offsets: n = %llu, plan has %llu frames + 1",
+                                   (unsigned long long)n, (unsigned long long)nfr);
+  (void)hipSetDevice(p->ctx->device);
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  static_assert(sizeof(unsigned long long) == sizeof(uint64_t), "u64");
+  HIPCHK(hipMemcpy(offsets, p->d_foff, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
   return FRA_OK;
 }
 
@@ -559,6 +585,47 @@ int fra_stream_header(uint8_t* o, int32_t channels, int32_t bps, int32_t sample_
   memcpy(vc + 8, kVendor, vlen);
   memset(vc + 8 + vlen, 0, 4);
   return FRA_OK;  // 42 + 4 + 40 = 86 bytes
+}
+
+int fra_normalize(fra_ctx* ctx, const void* data, int32_t on_device, int32_t dtype, uint64_t n, int32_t bps,
+                  const double* data_min, const double* data_max, void* out_host, double* mn_out, double* mx_out) {
+  if (!ctx || (!data && n) || (!out_host && n)) return set_err(FRA_E_INVALID, "null argument");
+  if (dtype < FRA_U8 || dtype > FRA_F64) return set_err(FRA_E_INVALID, "bad dtype %d", dtype);
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  const size_t in_bytes = (size_t)n * elem_size(dtype);
+  const size_t out_bytes = (size_t)n * (bps == 16 ? 2 : 4);
+  void* d_in = nullptr;
+  void* d_out = nullptr;
+  NormDev* d_nd = nullptr;
+  int rc = FRA_OK;
+  auto fail = [&](hipError_t e, const char* what) {
+    rc = set_err(FRA_E_HIP, "%s: %s", what, hipGetErrorString(e));
+  };
+  hipError_t e = hipSuccess;
+  if (!on_device && n) {
+    if ((e = hipMalloc(&d_in, in_bytes)) != hipSuccess) fail(e, "hipMalloc");
+    else if ((e = hipMemcpyAsync(d_in, data, in_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) fail(e, "h2d");
+  }
+  if (!rc && (e = hipMalloc(&d_out, std::max<size_t>(4, out_bytes))) != hipSuccess) fail(e, "hipMalloc");
+  if (!rc && (e = hipMalloc(&d_nd, sizeof(NormDev))) != hipSuccess) fail(e, "hipMalloc");
+  if (!rc && (e = launch_normalize_flat(dtype, on_device ? data : d_in, n, bps, d_nd, data_min != nullptr,
+                                        data_min ? *data_min : 0.0, data_max != nullptr, data_max ? *data_max : 0.0,
+                                        d_out, s)) != hipSuccess)
+    fail(e, "normalize kernels");
+  NormDev nd{};
+  if (!rc && out_bytes && (e = hipMemcpyAsync(out_host, d_out, out_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    fail(e, "d2h");
+  if (!rc && (e = hipMemcpyAsync(&nd, d_nd, sizeof(NormDev), hipMemcpyDeviceToHost, s)) != hipSuccess) fail(e, "d2h");
+  if (!rc && (e = hipStreamSynchronize(s)) != hipSuccess) fail(e, "sync");
+  if (!rc) {
+    if (mn_out) *mn_out = nd.mn;
+    if (mx_out) *mx_out = nd.mx;
+  }
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  (void)hipFree(d_nd);
+  return rc;
 }
 
 int fra_synth_raster(fra_ctx* ctx, int32_t kind, uint64_t seed, int32_t bands, int32_t height, int32_t width,

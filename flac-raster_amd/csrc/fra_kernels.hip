@@ -20,6 +20,8 @@
 // Numerics: compiled with -ffp-contract=off; every float/double expression on the decision path
 // is evaluated in exactly the order the oracle uses (IEEE add/mul/div are correctly rounded on
 // gfx950 and on x86-64, so identical op sequences give identical bits).
+#include <algorithm>
+
 #include "fra_device.h"
 
 namespace fra {
@@ -124,6 +126,86 @@ hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ============================================================================ fra_normalize (standalone a3)
+// normalize_to_audio of a flat (N, C) array, normalization.py:126-202.  Not on the encode path (the
+// encoder fuses this into k_analyze); IEEE division here because user-supplied data_min/data_max
+// overrides void the integer-range precondition of div_markstein.
+template <int SRC>
+__global__ void __launch_bounds__(256) k_minmax_flat(const void* data, uint64_t n, NormDev* nd) {
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const double v = load_f64<SRC>(data, (int64_t)i);
+    if (v == v) {
+      const unsigned long long k = okey(v);
+      kmin = k < kmin ? k : kmin;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned long long a = ((unsigned long long)__shfl_xor((uint32_t)(kmin >> 32), off, 64) << 32) |
+                                 __shfl_xor((uint32_t)kmin, off, 64);
+    const unsigned long long b = ((unsigned long long)__shfl_xor((uint32_t)(kmax >> 32), off, 64) << 32) |
+                                 __shfl_xor((uint32_t)kmax, off, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if ((threadIdx.x & 63) == 0 && kmin != ~0ull) {
+    atomicMin(&nd->mnkey, kmin);
+    atomicMax(&nd->mxkey, kmax);
+  }
+}
 
+__global__ void k_norm_finalize_flat(NormDev* nd, int has_min, double omin, int has_max, double omax) {
+  const double qnan = __longlong_as_double(0x7FF8000000000000ll);
+  const bool none = nd->mnkey == ~0ull;
+  const double mn = has_min ? omin : (none ? qnan : unkey(nd->mnkey));
+  const double mx = has_max ? omax : (none ? qnan : unkey(nd->mxkey));
+  nd->mn = mn;
+  nd->mx = mx;
+  nd->range = (mx <= mn) ? 1.0 : (mx - mn);  // normalization.py:154-159
+}
+
+template <int SRC>
+__global__ void __launch_bounds__(256) k_normalize_flat(const void* data, uint64_t n, const NormDev* nd, int bps,
+                                                        void* out) {
+  const double mn = nd->mn, range = nd->range;
+  const double scale = bps == 16 ? 32767.0 : (bps == 24 ? 8388607.0 : 2147483647.0);
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    double t = load_f64<SRC>(data, (int64_t)i) - mn;
+    t = 2.0 * t;
+    t = t / range;
+    t = t - 1.0;
+    if (t < -1.0) t = -1.0;
+    else if (t > 1.0) t = 1.0;
+    if (t != t) t = 0.0;
+    t = t * scale;
+    if (bps == 16) ((int16_t*)out)[i] = (int16_t)(int32_t)t;
+    else ((int32_t*)out)[i] = (int32_t)t;
+  }
+}
+
+hipError_t launch_normalize_flat(int src, const void* data, uint64_t n, int bps, NormDev* nd, int has_min, double omin,
+                                 int has_max, double omax, void* out, hipStream_t s) {
+  k_norm_init<<<1, 64, 0, s>>>(nd, 1);
+  const unsigned grid = (unsigned)std::min<uint64_t>(8192, std::max<uint64_t>(1, (n + 255) / 256));
+  if (!(has_min && has_max) && n) {
+    switch (src) {
+#define M(S_) case S_: k_minmax_flat<S_><<<grid, 256, 0, s>>>(data, n, nd); break;
+      FRA_SRC_CASES(M)
+#undef M
+      default: return hipErrorInvalidValue;
+    }
+  }
+  k_norm_finalize_flat<<<1, 1, 0, s>>>(nd, has_min, omin, has_max, omax);
+  if (n) {
+    switch (src) {
+#define M(S_) case S_: k_normalize_flat<S_><<<grid, 256, 0, s>>>(data, n, nd, bps, out); break;
+      FRA_SRC_CASES(M)
+#undef M
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return hipGetLastError();
+}
 
 }  // namespace fra

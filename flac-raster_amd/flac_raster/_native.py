@@ -53,12 +53,22 @@ class StreamInfo(C.Structure):
     ]
 
 
+class Decoded(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_int32), ("channels", C.c_int32), ("bps", C.c_int32), ("blocksize", C.c_int32),
+        ("nframes", C.c_int64), ("nsamples", C.c_uint64), ("nstreams", C.c_int32), ("audio_offset", C.c_uint64),
+    ]
+
+
+DECODE_CONCAT = 1
+
 EXPORTS = [
     "fra_last_error", "fra_abi_version", "fra_device_count", "fra_free", "fra_ctx_create", "fra_ctx_destroy",
     "fra_plan_create", "fra_plan_set_raster", "fra_plan_execute", "fra_plan_sync", "fra_plan_result",
     "fra_plan_download", "fra_plan_device_output", "fra_plan_enable_timing", "fra_plan_timing",
     "fra_plan_destroy", "fra_encode", "fra_stream_header", "fra_synth_raster", "fra_device_alloc",
-    "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d",
+    "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d", "fra_plan_frame_offsets", "fra_normalize",
+    "fra_decode",
 ]
 
 
@@ -101,6 +111,10 @@ def load():
         L.fra_device_free.argtypes = [vp, vp]
         L.fra_memcpy_d2h.argtypes = [vp, vp, vp, u64]
         L.fra_memcpy_h2d.argtypes = [vp, vp, vp, u64]
+        L.fra_plan_frame_offsets.argtypes = [vp, C.POINTER(u64), u64]
+        pd = C.POINTER(C.c_double)
+        L.fra_normalize.argtypes = [vp, vp, i32, i32, u64, i32, pd, pd, vp, pd, pd]
+        L.fra_decode.argtypes = [vp, u64, i32, C.POINTER(Decoded), C.POINTER(C.POINTER(C.c_int32))]
         _lib = L
         return L
 
@@ -161,6 +175,19 @@ class Context:
     def d2h(self, arr: np.ndarray, dev: int):
         _check(load().fra_memcpy_d2h(self.h, arr.ctypes.data_as(C.c_void_p), C.c_void_p(dev), arr.nbytes))
 
+    def normalize(self, data: np.ndarray, bps: int, data_min=None, data_max=None):
+        """normalize_to_audio on this context's GPU (fra_normalize).  Returns (audio, mn, mx)."""
+        a = np.ascontiguousarray(data)
+        if a.dtype not in DTYPE_CODES:
+            raise TypeError(f"unsupported dtype {a.dtype}")
+        out = np.empty(a.shape, dtype=np.int16 if bps == 16 else np.int32)
+        mn, mx = C.c_double(), C.c_double()
+        omin = C.byref(C.c_double(float(data_min))) if data_min is not None else None
+        omax = C.byref(C.c_double(float(data_max))) if data_max is not None else None
+        _check(load().fra_normalize(self.h, a.ctypes.data_as(C.c_void_p), 0, DTYPE_CODES[a.dtype], a.size, bps, omin,
+                                    omax, out.ctypes.data_as(C.c_void_p), C.byref(mn), C.byref(mx)))
+        return out, mn.value, mx.value
+
     def synth(self, kind: int, seed: int, bands: int, height: int, width: int, dev_out: int):
         _check(load().fra_synth_raster(self.h, kind, seed, bands, height, width, C.c_void_p(dev_out)))
 
@@ -213,6 +240,12 @@ class Plan:
         buf = np.empty(max(1, total), dtype=np.uint8)
         _check(load().fra_plan_download(self.h, buf.ctypes.data_as(C.c_void_p), total))
         return infos, buf[:total].tobytes()
+
+    def frame_offsets(self, nframes: int) -> np.ndarray:
+        """Byte offset of every frame in the concatenated output (+ total at the end)."""
+        off = np.empty(nframes + 1, dtype=np.uint64)
+        _check(load().fra_plan_frame_offsets(self.h, off.ctypes.data_as(C.POINTER(C.c_uint64)), nframes + 1))
+        return off
 
     def device_output(self) -> Tuple[int, int]:
         p, cap = C.c_void_p(), C.c_uint64()
@@ -276,9 +309,10 @@ def encode_windows(raster: np.ndarray, windows, level: int = 5, blocksize: int =
 
 
 def encode_interleaved(samples: np.ndarray, sample_rate: int, level: int = 5, blocksize: int = 4096,
-                       device: int = 0) -> Tuple[StreamInfo, bytes]:
+                       device: int = 0, return_offsets: bool = False):
     """pyflac ``StreamEncoder.process(samples); finish()`` semantics: samples (N, C) int16/int32
-    already in the audio domain; bps = itemsize*8.  Returns (info, frames)."""
+    already in the audio domain; bps = itemsize*8.  Returns (info, frames) or, with
+    ``return_offsets``, (info, frames, per-frame byte offsets + total)."""
     s = np.asarray(samples)
     if s.ndim == 1:
         s = s.reshape(-1, 1)
@@ -294,6 +328,23 @@ def encode_interleaved(samples: np.ndarray, sample_rate: int, level: int = 5, bl
         plan.execute()
         plan.sync()
         infos, data = plan.download()
+        if return_offsets:
+            return infos[0], data, plan.frame_offsets(infos[0].nframes)
         return infos[0], data
     finally:
         plan.close()
+
+def decode(data: bytes, concat: bool = False) -> Tuple[np.ndarray, Decoded]:
+    """Native FLAC decode (fra_decode; host code, no GPU needed).  Returns ((N, C) int32, info)."""
+    L = load()
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    info = Decoded()
+    ptr = C.POINTER(C.c_int32)()
+    _check(L.fra_decode(buf.ctypes.data_as(C.c_void_p), len(data), DECODE_CONCAT if concat else 0, C.byref(info),
+                        C.byref(ptr)))
+    try:
+        n = info.nsamples * info.channels
+        out = np.ctypeslib.as_array(ptr, shape=(max(1, n),))[:n].copy() if n else np.zeros(0, np.int32)
+    finally:
+        L.fra_free(ptr)
+    return out.reshape(-1, info.channels), info

@@ -1,0 +1,136 @@
+"""``--streaming`` container: ``[u32 BE index length][compact JSON index][tile FLAC streams]``.
+
+Writer = ``cli._create_streaming_flac`` (``cli.py:521-639``), the north-star path: per tile the
+reference writes a temp GeoTIFF, runs ``tiff_to_flac`` on it (normalise, pyflac, mutagen tags of
+the TILE: its size, transform, bounds, min/max) and appends the bytes.  Here all tiles are encoded
+by one batched GPU plan per device (``tiles.encode_tiles``), and the per-tile tag rewrite is the
+same host byte assembly (``flac_meta``) with the values the temp GeoTIFF would have carried:
+the window transform (rasterio ``windows.transform`` arithmetic), no nodata, the source CRS.
+
+Reader = the index parse + byte-range slicing of ``cli.extract`` (``cli.py:238-313``).
+"""
+
+from __future__ import annotations
+
+import json
+import struct
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import flac_meta
+from .converter import raster_metadata, raster_tags
+from .geo import Affine, window_transform
+from .tiff import GeoTIFF
+from .tiles import TileStream, calculate_tiles, encode_tiles
+
+
+def tile_flac_bytes(ts: TileStream, transform: Affine, crs: Optional[str], row_off: int, col_off: int, height: int,
+                    width: int, dtype) -> Tuple[bytes, Affine]:
+    """One tile's file as ``converter.tiff_to_flac(temp_tile.tif)`` would write it."""
+    tt = window_transform(transform, col_off, row_off)
+    md = raster_metadata(width, height, ts.channels, dtype, crs, tt, ts.data_min, ts.data_max, None,
+                         32767 if ts.bps == 16 else 8388607)
+    return flac_meta.rewrite_header(ts.data, raster_tags(md)), tt
+
+
+def assemble_streaming(tiles: Sequence[Tuple[int, int, int, int]], streams: Sequence[TileStream], shape,
+                       dtype, transform: Affine, crs: Optional[str], tile_size: int) -> bytes:
+    """Container bytes from encoded tile streams (tile order = ``calculate_tiles`` order)."""
+    B, H, W = shape
+    index: Dict = {"crs": str(crs), "transform": list(transform), "width": W, "height": H, "bands": B,
+                   "dtype": str(np.dtype(dtype)), "tile_size": tile_size, "frames": []}
+    chunks: List[bytes] = []
+    total = 0
+    for fid, ((r, c, h, w), ts) in enumerate(zip(tiles, streams)):
+        data, tt = tile_flac_bytes(ts, transform, crs, r, c, h, w, dtype)
+        xmin, ymax = tt.c, tt.f
+        index["frames"].append({
+            "frame_id": fid,
+            "bbox": [xmin, ymax + h * tt.e, xmin + w * tt.a, ymax],
+            "window": {"col_off": c, "row_off": r, "width": w, "height": h},
+            "byte_offset": total,
+            "byte_size": len(data),
+        })
+        chunks.append(data)
+        total += len(data)
+    head = json.dumps(index, separators=(",", ":")).encode("utf-8")
+    return len(head).to_bytes(4, "big") + head + b"".join(chunks)
+
+
+def build_streaming(raster: np.ndarray, transform: Affine, crs: Optional[str], tile_size: int,
+                    compression_level: int = 5, devices: Optional[Sequence[int]] = None) -> bytes:
+    """Container bytes for a band-planar ``(B, H, W)`` raster (all tiles on the GPU(s))."""
+    a = raster if raster.ndim == 3 else raster[None]
+    tiles = calculate_tiles(a.shape[1], a.shape[2], tile_size)
+    streams = encode_tiles(a, tiles, compression_level, devices)
+    return assemble_streaming(tiles, streams, a.shape, a.dtype, transform, crs, tile_size)
+
+
+def create_streaming_flac(input_path: Path, output_path: Path, tile_size: int = 512, compression_level: int = 5,
+                          devices: Optional[Sequence[int]] = None) -> Dict:
+    """Write the streaming container for a GeoTIFF; returns the index."""
+    g = GeoTIFF(input_path)
+    raster = g.read()
+    out = build_streaming(raster, Affine(*g.info.transform), g.info.crs, tile_size, compression_level, devices)
+    Path(output_path).write_bytes(out)
+    return read_index_bytes(out)[0]
+
+
+@dataclass
+class StreamingFile:
+    """Parsed container: index + absolute byte range of every tile."""
+
+    index: Dict
+    header_size: int
+
+    def tile_range(self, frame: Dict) -> Tuple[int, int]:
+        start = self.header_size + frame["byte_offset"]
+        return start, start + frame["byte_size"]
+
+
+def read_index_bytes(data: bytes) -> Tuple[Dict, int]:
+    n = struct.unpack(">I", data[:4])[0]
+    return json.loads(data[4:4 + n].decode("utf-8")), 4 + n
+
+
+def open_streaming(path: Path) -> StreamingFile:
+    with open(path, "rb") as f:
+        n = struct.unpack(">I", f.read(4))[0]
+        idx = json.loads(f.read(n).decode("utf-8"))
+    return StreamingFile(idx, 4 + n)
+
+
+def select_frame(frames: List[Dict], tile_id: Optional[int] = None, bbox: Optional[Sequence[float]] = None,
+                 center: bool = False, last: bool = False) -> Dict:
+    """Tile choice of ``cli.extract`` (``cli.py:245-296``)."""
+    if tile_id is not None:
+        fr = next((f for f in frames if f["frame_id"] == tile_id), None)
+        if fr is None:
+            raise KeyError(f"Tile ID {tile_id} not found")
+        return fr
+    if last:
+        return max(frames, key=lambda f: f["frame_id"])
+    if center:
+        boxes = [f["bbox"] for f in frames]
+        cx = (min(b[0] for b in boxes) + max(b[2] for b in boxes)) / 2
+        cy = (min(b[1] for b in boxes) + max(b[3] for b in boxes)) / 2
+        return min(frames, key=lambda f: ((f["bbox"][0] + f["bbox"][2]) / 2 - cx) ** 2
+                   + ((f["bbox"][1] + f["bbox"][3]) / 2 - cy) ** 2)
+    if bbox is not None:
+        if len(bbox) != 4:
+            raise ValueError("Bbox must have 4 coordinates")
+        hit = [f for f in frames if bbox[0] < f["bbox"][2] and bbox[2] > f["bbox"][0] and bbox[1] < f["bbox"][3]
+               and bbox[3] > f["bbox"][1]]
+        if not hit:
+            raise LookupError("No tiles intersect bbox")
+        return hit[0]
+    raise ValueError("Specify tile_id, bbox, center or last")
+
+
+def read_tile_bytes(path: Path, frame: Dict, header_size: int) -> bytes:
+    with open(path, "rb") as f:
+        f.seek(header_size + frame["byte_offset"])
+        return f.read(frame["byte_size"])

@@ -1,0 +1,134 @@
+"""Tile geometry and the batched GPU tile encoder shared by the streaming / spatial / standard paths.
+
+The reference encodes its units one at a time (``cli.py:553-622``: temp GeoTIFF per tile,
+``converter.tiff_to_flac``, mutagen; ``spatial_encoder.py:196-245``: ``_encode_tile_to_flac`` per
+tile).  Here every unit of a raster is one window of ONE plan (``fra_plan_*``): per-window
+nanmin/nanmax, normalisation, analysis, bit packing and CRCs run as a handful of kernel launches
+over all tiles at once.  With several devices, the tiles are split into contiguous runs of
+near-equal pixel count (so each device receives only the rows its tiles cover) and the devices
+run concurrently from host threads (ctypes releases the GIL); there is no exchange between
+devices.  Output is identical for any device count.
+"""
+
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native
+
+BLOCKSIZE = 4096  # converter.py:143, spatial_encoder.py:295
+
+
+def calculate_tiles(height: int, width: int, tile_size: int) -> List[Tuple[int, int, int, int]]:
+    """Row-major ``(row_off, col_off, h, w)`` with clipped edge tiles (``spatial_encoder.py:110-121``,
+    ``cli.py:553-556``)."""
+    if tile_size <= 0:
+        raise ValueError("tile_size must be positive")
+    return [(r, c, min(tile_size, height - r), min(tile_size, width - c))
+            for r in range(0, height, tile_size) for c in range(0, width, tile_size)]
+
+
+def split_contiguous(weights: Sequence[int], parts: int) -> List[Tuple[int, int]]:
+    """Split ``range(len(weights))`` into ``parts`` contiguous runs of near-equal total weight."""
+    n = len(weights)
+    parts = max(1, min(parts, n)) if n else 1
+    total = float(sum(weights))
+    out, start, acc = [], 0, 0.0
+    for p in range(parts - 1):
+        target = total * (p + 1) / parts
+        end = start
+        while end < n - (parts - 1 - p) and (acc + weights[end] <= target or end == start):
+            acc += weights[end]
+            end += 1
+        out.append((start, end))
+        start = end
+    out.append((start, n))
+    return out
+
+
+def lpt_assign(weights: Sequence[int], parts: int) -> List[List[int]]:
+    """Longest-processing-time assignment (used when data already lives on every device)."""
+    order = sorted(range(len(weights)), key=lambda i: (-weights[i], i))
+    loads = [0] * parts
+    groups: List[List[int]] = [[] for _ in range(parts)]
+    for i in order:
+        g = min(range(parts), key=lambda k: (loads[k], k))
+        groups[g].append(i)
+        loads[g] += weights[i]
+    return [sorted(g) for g in groups]
+
+
+@dataclass
+class TileStream:
+    """One encoded unit: a complete FLAC stream (86-byte header + frames) + its normalisation."""
+
+    data: bytes
+    data_min: float
+    data_max: float
+    sample_rate: int
+    bps: int        # FLAC bits per sample (16, or 32 for int32 audio: SURVEY.md F3)
+    channels: int
+    nframes: int
+
+
+def norm_bits(dtype) -> int:
+    """calculate_audio_params' bit depth: 16 for <=16-bit integers, else 24 (int32 audio)."""
+    return 16 if np.dtype(dtype) in (np.uint8, np.int8, np.uint16, np.int16) else 24
+
+
+def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int, device: int,
+                  norm: int, out: list, errors: list, slot: int):
+    try:
+        r0 = min(t[0] for t in tiles)
+        r1 = max(t[0] + t[2] for t in tiles)
+        sub = raster if (r0 == 0 and r1 == raster.shape[1]) else np.ascontiguousarray(raster[:, r0:r1, :])
+        wins = [(t[0] - r0, t[1], t[2], t[3]) for t in tiles]
+        infos, frames = _native.encode_windows(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
+                                               device=device)
+        res = []
+        mv = memoryview(frames)
+        for inf in infos:
+            hdr = _native.stream_header(inf.channels, inf.bps, inf.sample_rate, BLOCKSIZE)
+            body = mv[inf.offset:inf.offset + inf.frame_bytes]
+            res.append(TileStream(hdr + bytes(body), float(inf.data_min), float(inf.data_max), inf.sample_rate,
+                                  inf.bps, inf.channels, inf.nframes))
+        out[slot] = res
+    except BaseException as e:  # re-raised on the calling thread
+        errors.append(e)
+
+
+def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,
+                 devices: Optional[Sequence[int]] = None) -> List[TileStream]:
+    """Encode every tile of a band-planar ``(B, H, W)`` raster as its own FLAC stream on the GPU(s).
+
+    Each stream equals what ``normalize_to_audio`` + ``pyflac.StreamEncoder(blocksize=4096)``
+    produce for ``raster[:, r:r+h, c:c+w]`` interleaved pixel-major (``cli.py:557-597``).
+    """
+    a = np.asarray(raster)
+    if a.ndim == 2:
+        a = a[None]
+    if a.dtype not in _native.DTYPE_CODES:
+        raise TypeError(f"unsupported raster dtype {a.dtype}")
+    if not tiles:
+        return []
+    devs = list(devices) if devices else [0]
+    norm = norm_bits(a.dtype)
+    runs = split_contiguous([t[2] * t[3] for t in tiles], len(devs))
+    out: list = [None] * len(runs)
+    errors: list = []
+    if len(runs) == 1:
+        _encode_group(a, tiles, level, devs[0], norm, out, errors, 0)
+    else:
+        th = [threading.Thread(target=_encode_group, args=(a, tiles[s:e], level, devs[k], norm, out, errors, k))
+              for k, (s, e) in enumerate(runs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    if errors:
+        raise errors[0]
+    return [ts for grp in out for ts in grp]

@@ -111,6 +111,11 @@ FRA_API int fra_plan_result(fra_plan *plan, fra_stream_info *infos, uint64_t *to
 FRA_API int fra_plan_download(fra_plan *plan, uint8_t *host_out, uint64_t capacity);
 /* device pointer of the concatenated frames (valid until the next execute / destroy) */
 FRA_API int fra_plan_device_output(fra_plan *plan, const uint8_t **dev_ptr, uint64_t *capacity);
+/* after sync: byte offset of every frame of the concatenated output, frames of all windows in
+ * window order; offsets[nframes] = total bytes.  n must be sum(infos[].nframes) + 1.  This is what
+ * the pyflac-compatible shim needs to replay libFLAC's one-write-callback-per-frame sequence
+ * (docs/sonos-pyflac.txt:2311-2332). */
+FRA_API int fra_plan_frame_offsets(fra_plan *plan, uint64_t *offsets, uint64_t n);
 /* per-kernel timing with HIP events on the plan's stream: 0 minmax, 1 analyze, 2 frame-bytes+scan, 3 pack */
 FRA_API int fra_plan_enable_timing(fra_plan *plan, int32_t on);
 FRA_API int fra_plan_timing(fra_plan *plan, float *ms_sum4, int32_t *executes);
@@ -123,6 +128,32 @@ FRA_API int fra_encode(int device, const fra_job *job, uint8_t **out, uint64_t *
 /* fLaC + STREAMINFO(min=max blocksize, sizes 0, total samples 0, MD5 0) + VORBIS_COMMENT(vendor,
  * 0 comments, last) -- the 86-byte libFLAC 1.4.3 stream header layout. */
 FRA_API int fra_stream_header(uint8_t *out86, int32_t channels, int32_t bps, int32_t sample_rate, int32_t blocksize);
+
+/* normalize_to_audio (normalization.py:126-202) on the GPU for n elements of any dtype:
+ * mn = nanmin, mx = nanmax unless overridden (data_min / data_max non-NULL), R = mx - mn or 1.0 if
+ * mx <= mn, y = ((2.0*(x-mn))/R) - 1.0, clip[-1,1], NaN -> 0, then *32767 -> int16 (bps 16),
+ * *8388607 -> int32 (bps 24), *2147483647 -> int32 (any other bps), truncating.
+ * data: host or device (on_device) pointer; out_host: host buffer of n int16/int32.
+ * mn_out/mx_out receive the (possibly NaN) min/max actually used. */
+FRA_API int fra_normalize(fra_ctx *ctx, const void *data, int32_t on_device, int32_t dtype, uint64_t n, int32_t bps,
+                          const double *data_min, const double *data_max, void *out_host, double *mn_out,
+                          double *mx_out);
+
+/* Native FLAC decoder (read side; replaces pyflac.FileDecoder at
+ * converter.py:179-183): frame-parallel host decode of a complete stream (ID3v2 prefix allowed).
+ * *samples (malloc'ed, fra_free) receives nsamples x channels interleaved int32.  With
+ * FRA_DECODE_CONCAT, streams concatenated after the first one (the --spatial file layout,
+ * spatial_encoder.py:196-245) are appended if their format matches. Every CRC-8/CRC-16 is
+ * verified; a corrupt or truncated frame fails with FRA_E_INVALID. */
+#define FRA_DECODE_CONCAT 1
+typedef struct {
+  int32_t sample_rate, channels, bps, blocksize; /* STREAMINFO (blocksize = max blocksize) */
+  int64_t nframes;
+  uint64_t nsamples;                             /* per channel */
+  int32_t nstreams;
+  uint64_t audio_offset;                         /* first frame byte of the first stream */
+} fra_decoded;
+FRA_API int fra_decode(const uint8_t *data, uint64_t len, int32_t flags, fra_decoded *info, int32_t **samples);
 
 /* Synthetic rasters, generated on the device with integer-exact hashes so a
  * host numpy mirror reproduces any window bit for bit.  kind: 3 = C3 DEM int16, 4 = C4 S2-like

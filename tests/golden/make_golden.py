@@ -50,7 +50,7 @@ def main():
     norm = load_ref_normalization()
     meta = {"generator": "tests/golden/make_golden.py", "reference": "yharby/flac-raster@2026-02-27",
             "tiffs": {}, "audio_params": []}
-    for name in ["sample_rgb.tif", "sample_rgb.flac", "sample_dem.tif", "sample_multispectral.tif"]:
+    for name in ["sample_rgb.tif", "sample_rgb.flac", "sample_dem.tif", "sample_dem.flac", "sample_multispectral.tif"]:
         shutil.copyfile(REF / "test_data" / name, HERE / name)
 
     # --- sample TIFFs through interleave + reference normalize (converter.py:93-113)
@@ -104,7 +104,55 @@ def main():
             sr, bps = norm.calculate_audio_params(_Shape(shape), np.dtype(dt))
             meta["audio_params"].append({"dtype": dt, "shape": list(shape), "sample_rate": sr, "bps": bps})
     (HERE / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+    extra_vectors(norm)
     print("wrote", HERE)
+
+
+def extra_vectors(norm):
+    """normalize_to_audio with data_min/data_max overrides and the bps-32 fallback,
+    denormalize_from_audio (int16 / int32 / float64 PCM_16-style inputs) and
+    estimate_precision_loss -> normalize_extra.npz + precision_loss.json."""
+    import warnings
+    rng = np.random.default_rng(77)
+    vec = {}
+    x16 = rng.integers(0, 10000, size=3000).astype(np.uint16)
+    xf = rng.normal(0.2, 0.1, size=3000).astype(np.float32)
+    xi = rng.integers(-2**31, 2**31 - 1, size=3000, dtype=np.int64).astype(np.int32)
+    over = [("u16_override", x16, 16, 100.0, 9000.0), ("u16_override_lo", x16, 24, -5.5, None),
+            ("f32_override_hi", xf, 24, None, 0.25), ("i32_bps32", xi, 32, None, None),
+            ("u16_bps32", x16, 32, None, None), ("f32_inverted", xf, 16, 0.5, 0.1)]
+    for name, x, bps, lo, hi in over:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            a, p = norm.normalize_to_audio(x.reshape(-1, 1), bps, lo, hi)
+        vec[f"norm__{name}__in"] = x
+        vec[f"norm__{name}__out"] = a.reshape(-1)
+        vec[f"norm__{name}__args"] = np.array([bps, np.nan if lo is None else lo, np.nan if hi is None else hi,
+                                               p.data_min, p.data_max], dtype=np.float64)
+    cases = [
+        ("i16", rng.integers(-32767, 32768, size=2000).astype(np.int16), 100.0, 9000.0, "uint16", 16, 32767),
+        ("i16_i8", rng.integers(-32767, 32768, size=2000).astype(np.int16), -128.0, 127.0, "int8", 16, 32767),
+        ("i32", rng.integers(-8388607, 8388608, size=2000).astype(np.int32), -3.5, 1e6, "float32", 24, 8388607),
+        ("i32_u32", rng.integers(-8388607, 8388608, size=2000).astype(np.int32), 0.0, 4e9, "uint32", 24, 8388607),
+        ("f64_pcm16", rng.integers(-32768, 32768, size=2000).astype(np.float64) / 32768.0, 577.0, 1492.0,
+         "int16", 24, 8388607),
+        ("f64_float", rng.uniform(-1, 1, size=2000), 0.0, 0.4, "float64", 24, 8388607),
+    ]
+    for name, a, lo, hi, odt, bps, scale in cases:
+        p = norm.NormalizationParams(lo, hi, odt, bps, scale)
+        out = norm.denormalize_from_audio(a, p)
+        vec[f"denorm__{name}__in"] = a
+        vec[f"denorm__{name}__out"] = out
+        vec[f"denorm__{name}__params"] = np.array([lo, hi, bps, scale], dtype=np.float64)
+        vec[f"denorm__{name}__dtype"] = np.array(odt)
+    np.savez_compressed(HERE / "normalize_extra.npz", **vec)
+    rows = []
+    for dt in ["uint8", "int8", "uint16", "int16", "uint32", "int32", "float32", "float64"]:
+        for lo, hi in [(0.0, 255.0), (-1000.5, 30000.25), (0.0, 0.0), (577.0, 1492.0)]:
+            for bps in (16, 24, 32):
+                rows.append({"dtype": dt, "min": lo, "max": hi, "bps": bps,
+                             "out": norm.estimate_precision_loss(np.dtype(dt), lo, hi, bps)})
+    (HERE / "precision_loss.json").write_text(json.dumps(rows, indent=0))
 
 
 class _Shape:
@@ -117,4 +165,7 @@ class _Shape:
 
 
 if __name__ == "__main__":
-    main()
+    if "--extra-only" in sys.argv:
+        extra_vectors(load_ref_normalization())
+    else:
+        main()
