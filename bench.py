@@ -7,9 +7,11 @@ Workload (default ``--config c4``, the north-star configuration of BASELINE.json
 A *step* = one pass of the encode hot path over the whole scene: device-resident raster in HBM ->
 per-tile nanmin/nanmax -> normalize_to_audio -> FLAC analysis -> bit-packed frames of every tile
 in HBM (the bytes the reference's pyflac/libFLAC calls produce per tile, cli.py:553-622).
-Multi-GPU: tiles are sharded statically over ranks (LPT on pixel count); no
-collective on the data path; ``value`` = scene pixels / max-over-ranks step time (strong scaling:
-the scene is fixed, its tiles are split).
+Multi-GPU (one process per GPU, torch.distributed.run): weak scaling by default -- every rank
+encodes its own C4 scene (seed 20260227 + rank, generated in its HBM), i.e. the job is N scenes
+sharded one per GPU with no collective on the data path; ``value`` = pixels of all ranks' scenes /
+max-over-ranks time.  ``--scaling strong`` instead splits ONE scene's tiles over the ranks (LPT on
+pixel count).
 
 Also reported: ``roofline`` of the dominant kernel (HIP events on the plan's stream, algorithmic
 bytes = input raster bytes + emitted frame bytes of the units one launch processes), and
@@ -100,6 +102,7 @@ def main():
     ap.add_argument("--level", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.level is not None:
@@ -147,9 +150,10 @@ def main():
     dt = np.dtype(cfg["dtype"])
     raster_bytes = B * H * W * dt.itemsize
     dev_raster = ctx.alloc(raster_bytes)
-    ctx.synth(cfg["kind"], SEED, B, H, W, dev_raster)
+    weak = args.scaling == "weak"
+    ctx.synth(cfg["kind"], SEED + (rank if weak else 0), B, H, W, dev_raster)
     wins = tiles(H, W, cfg["tile"])
-    owner = lpt_shard(wins, world)
+    owner = [rank] * len(wins) if weak else lpt_shard(wins, world)
     mine = [i for i in range(len(wins)) if owner[i] == rank]
     my_wins = [wins[i] for i in mine]
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
@@ -195,7 +199,8 @@ def main():
     result = None
     if rank == 0:
         scene_px = H * W
-        value = scene_px * args.steps / T / 1e6
+        job_px = scene_px * (world if weak else 1)
+        value = job_px * args.steps / T / 1e6
         cpu = None
         if not args.no_cpu and world >= 1:
             _, frames = plan.download()
@@ -224,15 +229,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(T / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u16->i16 (int32 analysis, f64 autocorr)" if cfg["norm"] == 16 else "f32->i32 (int64 analysis)",
             "data": "synthetic (flac_raster.synth, seed 20260227; device-generated, integer-exact numpy mirror)",
             "config": {"workload": cfg["workload"], "level": cfg["level"], "tiles": len(wins),
                        "raster_bytes": raster_bytes, "compressed_bytes": int(out_bytes_all),
-                       "compression_ratio": round(raster_bytes / max(1.0, out_bytes_all), 4),
-                       "msamples_per_s": round(scene_px * B * args.steps / T / 1e6, 1),
-                       "parallelism": f"tiles sharded LPT over {world} GPU(s), no collective"},
+                       "compression_ratio": round(raster_bytes * (world if weak else 1) / max(1.0, out_bytes_all), 4),
+                       "msamples_per_s": round(job_px * B * args.steps / T / 1e6, 1),
+                       "parallelism": (f"{world} scene(s), one per GPU, no collective" if weak else
+                                       f"one scene's tiles sharded LPT over {world} GPU(s), no collective")},
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "alg_bytes_per_launch": int(alg_bytes),
