@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.level is not None:
@@ -211,6 +212,27 @@ def main():
                              f"scene through oracle/fr_oracle.c normalize+encode (FRA-1, 1 thread, "
                              f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}); "
                              f"bytes equal to GPU for {cb['checked'] - cb['mismatches']}/{cb['checked']} tiles"}
+        # PCIe-inclusive end-to-end (not `value`): host numpy raster -> H2D -> encode -> D2H frames
+        e2e = None
+        if not args.no_e2e:
+            host = np.empty((B, H, W), dtype=dt)
+            ctx.d2h(host, dev_raster)
+            p2 = N.Plan(ctx, host.ctypes.data, False, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"],
+                        keepalive=host)
+            p2.execute()
+            p2.download()
+            reps = 3
+            t0e = time.perf_counter()
+            for _ in range(reps):
+                p2.set_raster(host.ctypes.data, False, keepalive=host)
+                p2.execute()
+                _, fr2 = p2.download()
+            te = (time.perf_counter() - t0e) / reps
+            e2e = {"value": round(my_px / te / 1e6, 2), "unit": "MPix/s", "ms": round(te * 1e3, 2),
+                   "what": "pageable host raster -> H2D -> all kernels -> D2H of all frames (1 GPU)",
+                   "bytes_equal_device_path": bool(fr2 == plan.download()[1])}
+            p2.close()
+            del host
         # size vs libFLAC: only pinned for C2 (sample_rgb, 178,857 frame bytes at -c 5)
         size_c2 = None
         try:
@@ -249,6 +271,7 @@ def main():
                          "whole_path_gbps": round(path_gbps, 2)},
             "cpu_baseline": cpu,
             "size_ratio_vs_libflac_c2": size_c2,
+            "e2e": e2e,
         }
         print(json.dumps(result), flush=True)
     plan.close()
