@@ -40,7 +40,7 @@ struct AnalyzeSmem {
     uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
   } u;
   unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
-  double red[4][kMaxLpc + 1];
+  double red[2][4][kMaxLpc + 1];  // double-buffered by window parity
   double autoc[kMaxLpc + 1];
   double lp[kMaxLpc][kMaxLpc];
   double err[kMaxLpc];
@@ -293,28 +293,28 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++) {
           const double v = tree64(acc[l]);
-          if (lane == 63) S.red[wv][l] = v;
+          if (lane == 63) S.red[wi & 1][wv][l] = v;
         }
         __syncthreads();
+        // one lane: autocorrelation -> Levinson-Durbin -> order by expected bits (3.7) -> qlp.
+        // The other waves run ahead (next window / model sums); red[] is double-buffered and the
+        // next barrier is only passed once this lane is done.
         if (t == 0) {
-          for (int l = 0; l <= lmax; l++) S.autoc[l] = (S.red[0][l] + S.red[1][l]) + (S.red[2][l] + S.red[3][l]);
+          for (int l = 0; l <= lmax; l++)
+            S.autoc[l] = (S.red[wi & 1][0][l] + S.red[wi & 1][1][l]) + (S.red[wi & 1][2][l] + S.red[wi & 1][3][l]);
           int nord = 0;
           if (S.autoc[0] != 0.0) nord = levinson<MAXLAG>(S.autoc, lmax, S.lp, S.err);
-          int olo = 1, ohi = nord;
-          if (wi > 0 && nord > 0) { olo = ohi = best_order_by_error(S.err, nord, n, prec + sbps); }
-          S.nord = nord; S.olo = olo; S.ohi = ohi;
-        }
-        __syncthreads();
-        const int nord = S.nord, olo = S.olo, ohi = S.ohi;
-        if (nord > 0 && t < MAXLAG && olo + t <= ohi) {
-          const int o = olo + t;
-          const int m = wi == 0 ? 5 + o - 1 : 5 + kMaxLpc + wi - 1;
-          int32_t q[MAXLAG];
-          int sh = 0;
-          const bool ok = quantize<MAXLAG>(S.lp[o - 1], o, prec, q, sh);
-          S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh; S.mvalid[m] = ok ? 1 : 0;
+          const int m = 5 + wi;
+          S.mvalid[m] = 0;
+          if (nord > 0) {
+            const int o = best_order_by_error(S.err, nord, n, prec + sbps);
+            int32_t q[MAXLAG];
+            int sh = 0;
+            const bool ok = quantize<MAXLAG>(S.lp[o - 1], o, prec, q, sh);
+            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh; S.mvalid[m] = ok ? 1 : 0;
 #pragma unroll
-          for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
+            for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
+          }
         }
       }
     }
@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   }
   const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
   const int pidx0 = i0 < n ? i0 / psz : 0;
-  const int nmod = 5 + (MAXLAG > 0 ? kMaxLpc + a.nwin - 1 : 0);
+  const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
   if (fastframe) {
     if constexpr (!B32) {
       // FIXED 0..4 by finite differences (every fixed model is valid here: n >= 16)

@@ -24,7 +24,7 @@ constexpr int kChunk = 16;        // samples per thread (also the FRA-1 autocorr
 constexpr int kMaxLpc = 12;
 constexpr int kMaxPart = 64;      // 2^6 partitions (level 6-8 max partition order)
 constexpr int kMaxWin = 6;        // subdivide_tukey(3): 1 + 2 + 3 windows
-constexpr int kMaxModels = 5 + kMaxLpc + (kMaxWin - 1);  // fixed 0..4, window-0 orders, one per extra window
+constexpr int kMaxModels = 5 + kMaxWin;  // fixed 0..4, one LPC order per apodization window
 
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {

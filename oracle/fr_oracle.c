@@ -520,7 +520,7 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
   int bk[256];
   uint64_t best_est = 0;
 
-  /* candidate list: FIXED 0..4 then LPC orders of window 0 then one LPC per extra window */
+  /* candidate list: FIXED 0..4 then one LPC order per window */
   int fmax = n - 1 < 4 ? n - 1 : 4;
   for (int o = 0; o <= fmax; o++) {
     if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue; /* 32-bps: residual outside int32 */
@@ -543,8 +543,10 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
       if (!(autoc[0] != 0.0)) continue;
       double lp[32 * 32], err[32];
       int nord = ora_levinson(autoc, lmax, lp, err);
+      /* 3.7: one order per window, chosen by expected bits from the LD errors (libFLAC's
+       * non-exhaustive model search) */
       int olo = 1, ohi = nord;
-      if (wi > 0) { olo = ohi = best_order_by_error(err, nord, n, prec + sbps); }
+      if (nord > 0) { olo = ohi = best_order_by_error(err, nord, n, prec + sbps); }
       for (int o = olo; o <= ohi; o++) {
         int32_t q[32];
         int sh;
