@@ -173,7 +173,7 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
 }
 
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32> S;
   const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -296,22 +296,46 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
           if (lane == 63) S.red[wi & 1][wv][l] = v;
         }
         __syncthreads();
-        // one lane: autocorrelation -> Levinson-Durbin -> order by expected bits (3.7) -> qlp.
-        // The other waves run ahead (next window / model sums); red[] is double-buffered and the
-        // next barrier is only passed once this lane is done.
-        if (t == 0) {
-          for (int l = 0; l <= lmax; l++)
-            S.autoc[l] = (S.red[wi & 1][0][l] + S.red[wi & 1][1][l]) + (S.red[wi & 1][2][l] + S.red[wi & 1][3][l]);
-          int nord = 0;
-          if (S.autoc[0] != 0.0) nord = levinson<MAXLAG>(S.autoc, lmax, S.lp, S.err);
+        // wave 0, uniformly: autocorrelation -> Levinson-Durbin (registers) -> expected bits of every
+        // order in parallel (lane o) -> first minimum -> qlp quantisation.  The other waves run ahead
+        // (next window / model-sum setup); red[] is double-buffered and the next barrier is only
+        // passed once wave 0 is done.
+        if (wv == 0) {
+          double ac[MAXLAG + 1];
+#pragma unroll
+          for (int l = 0; l <= MAXLAG; l++)
+            ac[l] = l <= lmax ? (S.red[wi & 1][0][l] + S.red[wi & 1][1][l]) + (S.red[wi & 1][2][l] + S.red[wi & 1][3][l])
+                              : 0.0;
           const int m = 5 + wi;
-          S.mvalid[m] = 0;
+          int nord = 0;
+          double errv[MAXLAG];
+          if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp, errv, lane == 0);
+          bool ok = false;
+          int o = 0, sh = 0;
+          int32_t q[MAXLAG];
           if (nord > 0) {
-            const int o = best_order_by_error(S.err, nord, n, prec + sbps);
-            int32_t q[MAXLAG];
-            int sh = 0;
-            const bool ok = quantize<MAXLAG>(S.lp[o - 1], o, prec, q, sh);
-            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh; S.mvalid[m] = ok ? 1 : 0;
+            double e = errv[0];
+#pragma unroll
+            for (int j = 1; j < MAXLAG; j++)
+              if (lane == j + 1) e = errv[j];
+            const double bits = (lane >= 1 && lane <= nord) ? order_bits(e, n, lane, prec + sbps) : 0.0;
+            double best = __shfl(bits, 1, 64);
+            o = 1;
+            for (int oo = 2; oo <= nord; oo++) {
+              const double v = __shfl(bits, oo, 64);
+              if (v < best) { best = v; o = oo; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's lp rows -> all lanes
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            double lpo[MAXLAG];
+#pragma unroll
+            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[o - 1][j];
+            ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
+          }
+          if (lane == 0) {
+            S.mvalid[m] = ok ? 1 : 0;
+            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
 #pragma unroll
             for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
           }
@@ -336,15 +360,7 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
   if (fastframe) {
-    if constexpr (!B32) {
-      // FIXED 0..4 by finite differences (every fixed model is valid here: n >= 16)
-      uint64_t facc[5];
-      bool fovf[5];
-      fixed_sums_fast<false>(x, i0, facc, fovf);
-#pragma unroll
-      for (int k = 0; k <= 4; k++)
-        if (i0 < n && facc[k]) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)facc[k]);
-    } else {
+    if constexpr (B32) {
       // 32-bps: FIXED k as the 4-tap integer predictor (int64), one model at a time
       for (int m = 0; m < 5; m++) {
         const int o = m;
@@ -381,6 +397,23 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
       if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
       if constexpr (B32) {
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
+      }
+    }
+    if constexpr (!B32) {
+      // FIXED 0..4 by finite differences, in place (x is dead afterwards): after step k, x[j] for
+      // j >= 8 + k holds the k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.
+      // Same integers as the oracle's closed forms; every fixed model is valid here (n >= 16).
+#pragma unroll
+      for (int k = 0; k <= 4; k++) {
+        if (k > 0) {
+#pragma unroll
+          for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+        }
+        const int skip = k > i0 ? k - i0 : 0;
+        uint32_t s32 = 0;
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) s32 += jj >= skip ? zz32(x[12 + jj]) : 0u;
+        if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
       }
     }
   } else {
@@ -464,25 +497,41 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
   __syncthreads();
   unsigned long long(*esum)[3] = reinterpret_cast<unsigned long long(*)[3]>(&S.u.psum[0][0]);
   for (int i = t; i < kMaxPart * 3; i += kThreads) (&esum[0][0])[i] = 0ull;
-  __syncthreads();
+  // zig-zag residuals of the winner for this thread's 16 samples, computed ONCE: used by the exact
+  // Rice pass here and by the encoder below (0 for warm-up samples and past the block end)
+  uint32_t uu[kChunk];
   {
+    // reload the sample window from LDS (keeps the phase-4 window registers dead across the search)
+#pragma unroll
+    for (int j = 0; j < 12 + kChunk; j++) {
+      const int i = i0 - 12 + j;
+      x[j] = (i >= 0 && i < n) ? S.smp[i] : 0;
+    }
     int32_t q[MAXO];
 #pragma unroll
     for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+#pragma unroll
+    for (int jj = 0; jj < kChunk; jj++) {
+      const int i = i0 + jj;
+      const uint32_t uv = fastframe ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh))
+                                    : (i < n ? (uint32_t)zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh)) : 0u);
+      uu[jj] = (i < n && i >= o) ? uv : 0u;
+    }
+  }
+  __syncthreads();
+  {
     const int pz = n >> ps;
     uint64_t e0 = 0, e1 = 0, e2 = 0;
     if (fastframe) {
       const int pidx = i0 < n ? i0 / pz : 0;
       const int k = S.kpart[pidx];
-      const int skip = o > i0 ? o - i0 : 0;
+      const int km = k > 0 ? k - 1 : 0;  // e0 is only used when k >= 1
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
-        const uint64_t u = zz64(gres<B32, MAXO>(x, jj, q, sh));
-        if (jj >= skip) {
-          e0 += k > 0 ? (u >> (k - 1)) : 0ull;
-          e1 += u >> k;
-          e2 += u >> (k + 1);
-        }
+        const uint32_t u = uu[jj];
+        e0 += u >> km;
+        e1 += u >> k;
+        e2 += u >> (k + 1);
       }
       if (i0 < n) {
         atomicAdd(&esum[pidx][0], (unsigned long long)e0);
@@ -503,8 +552,11 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
           pend = (pidx + 1) * pz;
           k = S.kpart[pidx];
         }
-        const uint64_t u = zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh));
-        e0 += k > 0 ? (u >> (k - 1)) : 0ull;
+        uint32_t u = 0;
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++)
+          if (i - i0 == jj) u = uu[jj];
+        e0 += k > 0 ? (u >> (k - 1)) : 0u;
         e1 += u >> k;
         e2 += u >> (k + 1);
       }
@@ -582,27 +634,20 @@ __global__ void __launch_bounds__(kThreads) k_analyze(JobArgs a, int src) {
     }
     if (t == 0) lds_put(buf, pos, ((uint32_t)S.fmethod << 4) | (uint32_t)ps, 6);
     pos += 6;
-    int32_t q[MAXO];
-#pragma unroll
-    for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
     const int pz = n >> ps;
-    uint32_t uu[kChunk], kk[kChunk];  // zig-zag residual; Rice parameter | partition-start << 8
+    uint32_t kk[kChunk];  // Rice parameter | partition-start << 8, 0xFFFF = no code
     uint32_t tot = 0;
     int pidx = i0 < n ? i0 / pz : 0, pend = (pidx + 1) * pz;
     int kcur = S.kfin[pidx];
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) {
       const int i = i0 + jj;
-      uu[jj] = 0;
       kk[jj] = 0xFFFFu;
-      const uint32_t uv = fastframe ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh))
-                                    : (i < n ? (uint32_t)zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh)) : 0u);
       if (i < n && i >= o) {
         if (i >= pend) { pidx++; pend += pz; kcur = S.kfin[pidx]; }
         const bool pstart = (pidx == 0) ? (i == o) : (i == pidx * pz);
-        uu[jj] = uv;
         kk[jj] = (uint32_t)kcur | (pstart ? 0x100u : 0u);
-        tot += (uv >> kcur) + 1u + (uint32_t)kcur + (pstart ? (uint32_t)pb : 0u);
+        tot += (uu[jj] >> kcur) + 1u + (uint32_t)kcur + (pstart ? (uint32_t)pb : 0u);
       }
     }
     const uint32_t inc = wave_incl_scan32(tot);

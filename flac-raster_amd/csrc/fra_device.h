@@ -285,8 +285,11 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // ---------------------------------------------------------------- LPC analysis helpers
-// deterministic log2 -- same op sequence as oracle ora_det_log2
+// deterministic log2 -- same op sequence as oracle ora_det_log2 (series terms
+// multiplied by the correctly rounded constants 1/(2k+1); the only division is t)
 __device__ inline double det_log2(double x) {
+  constexpr double kInvOdd[12] = {1.0,      1.0 / 3,  1.0 / 5,  1.0 / 7,  1.0 / 9,  1.0 / 11,
+                                  1.0 / 13, 1.0 / 15, 1.0 / 17, 1.0 / 19, 1.0 / 21, 1.0 / 23};
   int e;
   double m = frexp(x, &e);
   m = m * 2.0;
@@ -294,29 +297,74 @@ __device__ inline double det_log2(double x) {
   const double t = (m - 1.0) / (m + 1.0);
   const double t2 = t * t;
   double sum = 0.0, p = t;
+#pragma unroll
   for (int k = 0; k < 12; k++) {
-    sum = sum + p / (double)(2 * k + 1);
+    sum = sum + p * kInvOdd[k];
     p = p * t2;
   }
   return (double)e + 2.0 * sum * 1.4426950408889634;
+}
+// expected bits of LPC order o from its LD error (== oracle best_order_by_error's per-order term)
+__device__ inline double order_bits(double e, int n, int o, int overhead) {
+  double bps;
+  if (e > 0.0) {
+    bps = 0.5 * det_log2(0.5 * e / (double)n);
+    if (bps < 0.0) bps = 0.0;
+  } else if (e < 0.0) bps = 1e32;
+  else bps = 0.0;
+  return bps * (double)(n - o) + (double)(o * overhead);
 }
 __device__ inline int best_order_by_error(const double* err, int norders, int n, int overhead) {
   double best = 0.0;
   int bo = 1;
   for (int o = 1; o <= norders; o++) {
-    const double e = err[o - 1];
-    double bps;
-    if (e > 0.0) {
-      bps = 0.5 * det_log2(0.5 * e / (double)n);
-      if (bps < 0.0) bps = 0.0;
-    } else if (e < 0.0) bps = 1e32;
-    else bps = 0.0;
-    const double bits = bps * (double)(n - o) + (double)(o * overhead);
+    const double bits = order_bits(err[o - 1], n, o, overhead);
     if (o == 1 || bits < best) { best = bits; bo = o; }
   }
   return bo;
 }
 
+// Levinson-Durbin run uniformly by a whole wave from register-resident autocorrelation: errors
+// stay in registers (errv), coefficient rows go to LDS from lane 0 only.  Same op sequence as
+// oracle ora_levinson.
+template <int MAXLAG>
+__device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_order, double (*lp)[kMaxLpc],
+                                    double (&errv)[MAXLAG], bool writer) {
+  double lpc[MAXLAG];
+#pragma unroll
+  for (int j = 0; j < MAXLAG; j++) { lpc[j] = 0.0; errv[j] = 0.0; }
+  double err = ac[0];
+  int result = max_order;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < MAXLAG; i++) {
+    if (!done && i < max_order) {
+      double r = -ac[i + 1];
+#pragma unroll
+      for (int j = 0; j < i; j++) r = r - lpc[j] * ac[i - j];
+      r = r / err;
+      lpc[i] = r;
+#pragma unroll
+      for (int j = 0; j < (i >> 1); j++) {
+        const double tmp = lpc[j];
+        lpc[j] = lpc[j] + r * lpc[i - 1 - j];
+        lpc[i - 1 - j] = lpc[i - 1 - j] + r * tmp;
+      }
+      if (i & 1) lpc[i >> 1] = lpc[i >> 1] + lpc[i >> 1] * r;
+      err = err * (1.0 - r * r);
+      if (writer) {
+#pragma unroll
+        for (int j = 0; j <= i; j++) lp[i][j] = -lpc[j];
+      }
+      errv[i] = err;
+      if (!(err > 0.0)) {
+        result = (err == 0.0) ? i + 1 : i;
+        done = true;
+      }
+    }
+  }
+  return result;
+}
 // Levinson-Durbin, same op sequence as oracle ora_levinson; loops unrolled to the
 // compile-time bound so the recursion state stays in registers.
 template <int MAXLAG>

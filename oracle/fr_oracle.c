@@ -318,7 +318,10 @@ ORA_API int ora_quantize(const double *lp, int order, int precision, int32_t *q,
 
 static int bitlen_u64(uint64_t v) { int b = 0; while (v) { b++; v >>= 1; } return b; }
 
-/* deterministic log2 (frexp + atanh series), DESIGN.md 3.7 */
+/* deterministic log2 (frexp + atanh series with the constant reciprocals 1/(2k+1) correctly rounded
+ * to double, so no division inside the series), DESIGN.md 3.7 */
+static const double INV_ODD[12] = {1.0,      1.0 / 3,  1.0 / 5,  1.0 / 7,  1.0 / 9,  1.0 / 11,
+                                   1.0 / 13, 1.0 / 15, 1.0 / 17, 1.0 / 19, 1.0 / 21, 1.0 / 23};
 ORA_API double ora_det_log2(double x) {
   int e;
   double m = frexp(x, &e);
@@ -328,7 +331,7 @@ ORA_API double ora_det_log2(double x) {
   double t2 = t * t;
   double sum = 0.0, p = t;
   for (int k = 0; k < 12; k++) {
-    sum = sum + p / (double)(2 * k + 1);
+    sum = sum + p * INV_ODD[k];
     p = p * t2;
   }
   return (double)e + 2.0 * sum * 1.4426950408889634;
