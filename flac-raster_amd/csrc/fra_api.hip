@@ -26,7 +26,8 @@
 #include "fra_internal.h"
 
 namespace fra {
-hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, hipStream_t s);
+hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, int vec_bytes, int rows, int max_rows,
+                         hipStream_t s);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
@@ -70,6 +71,7 @@ struct fra_plan {
   bool b32 = false;
   int nwin = 0;
   int max_segs = 0;
+  int mm_vec = 0, mm_rows = 1, mm_max_rows = 0;  // vectorised k_minmax shape (0 = scalar path)
   int cmax = 1;
   size_t raster_bytes = 0;
   // device buffers
@@ -304,6 +306,29 @@ static int plan_build(fra_plan* p) {
     nf_total += nfr;
     p->streams.push_back(st);
   }
+  // vectorised min/max: every window start, row, band and width a multiple of V = vec/itemsize
+  p->mm_vec = 0;
+  if (j.norm != 0 && j.col_stride == 1 && elem_size(j.dtype) <= 4) {
+    for (int vb : {16, 8}) {
+      const int64_t V = vb / elem_size(j.dtype);
+      bool ok = V >= 2 && j.row_stride % V == 0 && (j.channels == 1 || j.band_stride % V == 0);
+      int64_t max_nv = 1;
+      for (int w = 0; ok && w < j.nwindows; w++) {
+        const StreamDev& st = p->streams[w];
+        if (st.nsamples == 0) continue;
+        ok = st.base_off % V == 0 && st.width % V == 0 && st.width / V <= 65535;
+        max_nv = std::max<int64_t>(max_nv, st.width / V);
+      }
+      if (!ok) continue;
+      const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(64, 2048 / max_nv));
+      if (rows * max_nv * max_nv >= (int64_t(1) << 32)) continue;
+      p->mm_vec = vb;
+      p->mm_rows = (int)rows;
+      p->mm_max_rows = 0;
+      for (const StreamDev& st : p->streams) p->mm_max_rows = std::max(p->mm_max_rows, (int)st.height);
+      break;
+    }
+  }
   if (nf_total > INT32_MAX / 2) return set_err(FRA_E_INVALID, "too many frames (%lld)", (long long)nf_total);
   p->raster_bytes = (size_t)max_extent * elem_size(j.dtype);
   p->out_cap = out_cap + 64;
@@ -430,7 +455,8 @@ int fra_plan_execute(fra_plan* p) {
   const int nstreams = (int)p->streams.size();
   if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));
   if (p->job.norm != 0 && nstreams > 0 && p->max_segs > 0) {
-    HIPCHK(launch_minmax(p->src, a, nstreams, p->max_segs, s));
+    const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
+    HIPCHK(launch_minmax(p->src, a, nstreams, p->max_segs, vec, p->mm_rows, p->mm_max_rows, s));
     HIPCHK(launch_norm_finalize(a, nstreams, s));
   }
   if (p->timing) HIPCHK(hipEventRecord(p->ev[1], s));

@@ -81,6 +81,90 @@ __global__ void __launch_bounds__(256) k_minmax(const void* raster, const Stream
   }
 }
 
+// Vectorised variant (the plan's hot path): grid x = block of `rows` window rows, y = stream.
+// Each lane loads V consecutive elements with one aligned vector load (the host checks that every
+// window start, row, band and window width are multiples of V and that the raster pointer is
+// aligned); the (row, vector) pairs of a band are spread over the whole block, 8 loads in flight
+// per thread.  Per element: a 32-bit ordered key (integers: value / sign-flipped, f32: IEEE order
+// key, NaN skipped) -- the same total order as okey() on the float64 value, so the result equals
+// k_minmax's.
+template <typename T, int V>
+struct alignas(sizeof(T) * V) VecT {
+  T v[V];
+};
+template <int SRC>
+__device__ __forceinline__ uint32_t key32(typename RawType<SRC>::T x, bool& ok) {
+  if constexpr (SRC == ST_U8 || SRC == ST_U16 || SRC == ST_U32) {
+    ok = true;
+    return (uint32_t)x;
+  } else if constexpr (SRC == ST_I8 || SRC == ST_I16 || SRC == ST_I32) {
+    ok = true;
+    return (uint32_t)(int32_t)x ^ 0x80000000u;
+  } else {  // ST_F32
+    const uint32_t b = __float_as_uint(x);
+    ok = x == x;
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+  }
+}
+template <int SRC>
+__device__ __forceinline__ double unkey32(uint32_t k) {
+  if constexpr (SRC == ST_U8 || SRC == ST_U16 || SRC == ST_U32) return (double)k;
+  else if constexpr (SRC == ST_I8 || SRC == ST_I16 || SRC == ST_I32) return (double)(int32_t)(k ^ 0x80000000u);
+  else return (double)__uint_as_float((k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
+}
+template <int SRC, int V>
+__global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const StreamDev* streams, NormDev* nd,
+                                                    int rows) {
+  using T = typename RawType<SRC>::T;
+  using VT = VecT<T, V>;
+  constexpr int U = 8;
+  const StreamDev st = streams[blockIdx.y];
+  if (st.norm == 0) return;
+  const int r0 = blockIdx.x * rows;
+  if (r0 >= st.height) return;
+  const int nr = min(st.height - r0, rows);
+  const uint32_t nv = (uint32_t)(st.width / V);
+  const uint32_t E = (uint32_t)nr * nv;  // (row, vector) items per band
+  // idx / nv by multiply-high: exact while E * nv < 2^32 (checked on the host)
+  const uint32_t magic = 0xFFFFFFFFu / nv + 1u;
+  uint32_t kmin = ~0u, kmax = 0u;
+  for (int b = 0; b < st.channels; b++) {
+    const T* base = (const T*)raster + st.base_off + (int64_t)b * st.band_stride + (int64_t)r0 * st.row_stride;
+    for (uint32_t i0 = 0; i0 < E; i0 += 256 * U) {
+      VT x[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {  // items past E re-read item E-1 (idempotent for min/max)
+        const uint32_t idx = min(i0 + (uint32_t)(u * 256) + threadIdx.x, E - 1);
+        const uint32_t r = __umulhi(idx, magic), v = idx - r * nv;
+        x[u] = *(const VT*)(base + (int64_t)r * st.row_stride + (int64_t)v * V);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+#pragma unroll
+        for (int e = 0; e < V; e++) {
+          bool ok;
+          const uint32_t k = key32<SRC>(x[u].v[e], ok);
+          kmin = ok ? min(kmin, k) : kmin;
+          kmax = ok ? max(kmax, k) : kmax;
+        }
+      }
+    }
+  }
+  kmin = wave_min32(kmin);
+  kmax = ~wave_min32(~kmax);
+  __shared__ uint32_t smn[4], smx[4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[wv] = kmin; smx[wv] = kmax; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) { kmin = min(kmin, smn[w]); kmax = max(kmax, smx[w]); }
+    if (kmin <= kmax) {  // at least one non-NaN value
+      atomicMin(&nd[blockIdx.y].mnkey, okey(unkey32<SRC>(kmin)));
+      atomicMax(&nd[blockIdx.y].mxkey, okey(unkey32<SRC>(kmax)));
+    }
+  }
+}
+
 __global__ void k_frame_bytes(JobArgs a) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g > a.nframes_total) return;
@@ -109,8 +193,24 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, hipStream_t s) {
+// vec_bytes = 16 or 8: vector path (host-checked alignment), rows/max_rows its block shape; 0: scalar
+hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, int vec_bytes, int rows, int max_rows,
+                         hipStream_t s) {
   k_norm_init<<<(nstreams + 255) / 256, 256, 0, s>>>(a.norm, nstreams);
+  if (vec_bytes == 16 || vec_bytes == 8) {
+    dim3 vgrid((unsigned)((max_rows + rows - 1) / rows), (unsigned)nstreams);
+#define V(S_, T_)                                                                               \
+  case S_:                                                                                      \
+    if (vec_bytes == 16) k_minmax_vec<S_, 16 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows); \
+    else k_minmax_vec<S_, 8 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows);                  \
+    return hipGetLastError();
+    switch (src) {
+      V(ST_U8, uint8_t) V(ST_I8, int8_t) V(ST_U16, uint16_t) V(ST_I16, int16_t)
+      V(ST_U32, uint32_t) V(ST_I32, int32_t) V(ST_F32, float)
+      default: break;  // f64: scalar path
+    }
+#undef V
+  }
   dim3 grid((unsigned)max_segs, (unsigned)nstreams);
   switch (src) {
 #define M(S_) case S_: k_minmax<S_><<<grid, 256, 0, s>>>(a.raster, a.streams, a.norm); break;
