@@ -34,7 +34,7 @@ constexpr int buf_words() { return B32 ? kMaxBlock + 16 : kMaxBlock / 2 + 16; }
 
 template <bool B32>
 struct AnalyzeSmem {
-  int32_t smp[kMaxBlock];
+  int32_t smp[kSmpWords];  // sample i at sidx(i); words [0, kSmpStride) = zero chunk
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
     uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
@@ -196,6 +196,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 #endif
 
   // ---- 1. load + normalise
+  if (t < kSmpStride) S.smp[t] = 0;  // zero chunk (samples before the block start)
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   {
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
   if (w) {
-    for (int i = t; i < n; i += kThreads) S.smp[i] = S.smp[i] >> w;
+    for (int i = t; i < n; i += kThreads) S.smp[sidx(i)] = S.smp[sidx(i)] >> w;
     __syncthreads();
   }
   const uint32_t hdr = 8u + (uint32_t)(w ? w : 0);
@@ -267,7 +268,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 #pragma unroll
         for (int j = 0; j < kChunk + MAXLAG; j++) {
           const int i = i0 + j;
-          wf[j] = (i < n) ? (float)S.smp[i] * win[i] : 0.0f;
+          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * win[i] : 0.0f;
         }
         // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
         // float*float product, so this is bit-identical to the oracle's acc + a*b
@@ -350,12 +351,13 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   const int psz = n >> P;
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
   __syncthreads();
+  // x[j] = sample i0 - 12 + j: the last 12 of the previous chunk (the zero chunk for thread 0) and
+  // this thread's 16 (samples past n are never counted: their sums/codes are masked by i0 < n / i < n)
   int32_t x[12 + kChunk];
 #pragma unroll
-  for (int j = 0; j < 12 + kChunk; j++) {
-    const int i = i0 - 12 + j;
-    x[j] = (i >= 0 && i < n) ? S.smp[i] : 0;
-  }
+  for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+#pragma unroll
+  for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
   const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
@@ -503,10 +505,9 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   {
     // reload the sample window from LDS (keeps the phase-4 window registers dead across the search)
 #pragma unroll
-    for (int j = 0; j < 12 + kChunk; j++) {
-      const int i = i0 - 12 + j;
-      x[j] = (i >= 0 && i < n) ? S.smp[i] : 0;
-    }
+    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+#pragma unroll
+    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
     int32_t q[MAXO];
 #pragma unroll
     for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
@@ -619,10 +620,10 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
   }
   if (ftype == 1) {
-    for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[i] & smask, sbps);
+    for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
   } else {
     const int pb = S.fmethod ? 5 : 4;
-    for (int i = t; i < o; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[i] & smask, sbps);
+    for (int i = t; i < o; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
     uint32_t pos = hdr + (uint32_t)o * sbps;
     if (ftype == 3) {
       if (t == 0) {

@@ -149,7 +149,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       int32_t v;
       if (np.mode == 0) v = (int32_t)raw[k];
       else v = norm_sample<SRC>((double)raw[k], np);
-      smp[i] = v;
+      smp[sidx(i)] = v;
       orv |= (uint32_t)v;
       vmin = min(vmin, v);
       vmax = max(vmax, v);
@@ -533,12 +533,12 @@ template <bool B32, int MAXO>
 __device__ __forceinline__ int64_t gres_lds(const int32_t* smp, int i, const int32_t* q, int sh) {
   if constexpr (B32) {
     int64_t sum = 0;
-    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[max(0, i - 1 - j)];
-    return (int64_t)smp[i] - (sum >> sh);
+    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[sidx(max(0, i - 1 - j))];
+    return (int64_t)smp[sidx(i)] - (sum >> sh);
   } else {
     int32_t sum = 0;
-    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], smp[max(0, i - 1 - j)]);
-    return (int64_t)(smp[i] - (sum >> sh));
+    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], smp[sidx(max(0, i - 1 - j))]);
+    return (int64_t)(smp[sidx(i)] - (sum >> sh));
   }
 }
 

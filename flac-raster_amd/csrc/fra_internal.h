@@ -25,6 +25,12 @@ constexpr int kMaxLpc = 12;
 constexpr int kMaxPart = 64;      // 2^6 partitions (level 6-8 max partition order)
 constexpr int kMaxWin = 6;        // subdivide_tukey(3): 1 + 2 + 3 windows
 constexpr int kMaxModels = 5 + kMaxWin;  // fixed 0..4, one LPC order per apodization window
+// LDS sample array layout of k_analyze: each thread's 16-sample chunk at a stride of 20 words (4 pad
+// words), so the per-thread chunk reads (lane stride 20 dwords) are bank-conflict free for
+// ds_read_b32..b128; one zeroed chunk in front stands in for the samples before the block start.
+constexpr int kSmpStride = kChunk + 4;
+constexpr int kSmpWords = (kMaxBlock / kChunk + 1) * kSmpStride;
+FRA_HD int sidx(int i) { return kSmpStride + i + ((i >> 4) << 2); }
 
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {
