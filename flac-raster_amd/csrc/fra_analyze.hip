@@ -97,6 +97,19 @@ __device__ __forceinline__ uint64_t lpc_sum_fast(const int32_t* x, const int32_t
   return acc;
 }
 
+// 16-bit path: sum of zig-zag LPC residuals of the thread's 16 samples in 32 bits (|r| < 2^27, see
+// acc_zz); the warm-up positions jj < O are masked for thread 0 only (compile-time bound)
+template <int O>
+__device__ __forceinline__ uint64_t lpc_sum16(const int32_t* x, const int32_t* q, int sh, bool head) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int jj = 0; jj < kChunk; jj++) {
+    const uint32_t u = zz32((int32_t)gres<false, O>(x, jj, q, sh));
+    acc += (jj < O && head) ? 0u : u;
+  }
+  return acc;
+}
+
 // Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at
 // lane 2^p + j (level P = 6 nodes in a second register), so each lane runs ONE Rice estimate and
 // the per-level totals come out of a single upper-lane DPP chain (level p's segment is the aligned
@@ -359,6 +372,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 #pragma unroll
   for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
   const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
+  const bool head = i0 == 0;                    // this thread holds the warm-up samples (order <= 12 < 16)
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
   if (fastframe) {
@@ -390,7 +404,10 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       switch (o) {
 #define FRA_CASE(O_) \
   case O_:           \
-    if constexpr (O_ <= MAXO) acc = lpc_sum_fast<B32, O_>(x, q, sh, skip, ovf); \
+    if constexpr (O_ <= MAXO) { \
+      if constexpr (B32) acc = lpc_sum_fast<B32, O_>(x, q, sh, skip, ovf); \
+      else acc = lpc_sum16<O_>(x, q, sh, head); \
+    } \
     break;
         FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6)
         FRA_CASE(7) FRA_CASE(8) FRA_CASE(9) FRA_CASE(10) FRA_CASE(11) FRA_CASE(12)
@@ -411,10 +428,10 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 #pragma unroll
           for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
         }
-        const int skip = k > i0 ? k - i0 : 0;
+        // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
         uint32_t s32 = 0;
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) s32 += jj >= skip ? zz32(x[12 + jj]) : 0u;
+        for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
         if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
       }
     }
@@ -500,22 +517,48 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   unsigned long long(*esum)[3] = reinterpret_cast<unsigned long long(*)[3]>(&S.u.psum[0][0]);
   for (int i = t; i < kMaxPart * 3; i += kThreads) (&esum[0][0])[i] = 0ull;
   // zig-zag residuals of the winner for this thread's 16 samples, computed ONCE: used by the exact
-  // Rice pass here and by the encoder below (0 for warm-up samples and past the block end)
+  // Rice pass here and by the encoder below.  Slow frames: 0 for warm-up samples and past the block
+  // end; fast frames: warm-up samples 0, samples past the block end (threads with i0 >= n) unused.
   uint32_t uu[kChunk];
-  {
+  uint32_t fs[3] = {0u, 0u, 0u};  // fast frames: this thread's sums of u >> (k0-1), u >> k0, u >> (k0+1)
+  if (fastframe) {
     // reload the sample window from LDS (keeps the phase-4 window registers dead across the search)
 #pragma unroll
     for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
 #pragma unroll
     for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+    if (!B32 && type == 2) {
+      // FIXED winner: the o-th finite difference in place (wave-uniform o), as in phase 4
+#pragma unroll
+      for (int k = 1; k <= 4; k++) {
+        if (k <= o) {
+#pragma unroll
+          for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj]);
+    } else {
+      int32_t q[MAXO];
+#pragma unroll
+      for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++)
+        uu[jj] = B32 ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh)) : zz32((int32_t)gres<B32, MAXO>(x, jj, q, sh));
+    }
+    if (head) {
+#pragma unroll
+      for (int jj = 0; jj < 12; jj++)
+        if (jj < o) uu[jj] = 0u;
+    }
+  } else {
     int32_t q[MAXO];
 #pragma unroll
     for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) {
       const int i = i0 + jj;
-      const uint32_t uv = fastframe ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh))
-                                    : (i < n ? (uint32_t)zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh)) : 0u);
+      const uint32_t uv = i < n ? (uint32_t)zz64(gres_lds<B32, MAXO>(S.smp, i, q, sh)) : 0u;
       uu[jj] = (i < n && i >= o) ? uv : 0u;
     }
   }
@@ -527,12 +570,23 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       const int pidx = i0 < n ? i0 / pz : 0;
       const int k = S.kpart[pidx];
       const int km = k > 0 ? k - 1 : 0;  // e0 is only used when k >= 1
+      if constexpr (B32) {
 #pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) {
-        const uint32_t u = uu[jj];
-        e0 += u >> km;
-        e1 += u >> k;
-        e2 += u >> (k + 1);
+        for (int jj = 0; jj < kChunk; jj++) {
+          const uint32_t u = uu[jj];
+          e0 += u >> km;
+          e1 += u >> k;
+          e2 += u >> (k + 1);
+        }
+      } else {  // u < 2^28 on the 16-bit path: 16 of them fit 32 bits
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) {
+          const uint32_t u = uu[jj];
+          fs[0] += u >> km;
+          fs[1] += u >> k;
+          fs[2] += u >> (k + 1);
+        }
+        e0 = fs[0]; e1 = fs[1]; e2 = fs[2];
       }
       if (i0 < n) {
         atomicAdd(&esum[pidx][0], (unsigned long long)e0);
@@ -636,6 +690,34 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     if (t == 0) lds_put(buf, pos, ((uint32_t)S.fmethod << 4) | (uint32_t)ps, 6);
     pos += 6;
     const int pz = n >> ps;
+    if (!B32 && fastframe) {
+      // one partition per thread: Rice parameter kcur for all 16 codes, code bits from the exact-pass
+      // sums (kcur is k0-1, k0 or k0+1), the partition parameter in front of the thread's first code
+      const bool live = i0 < n;
+      const int pidx = live ? i0 / pz : 0;
+      const int kcur = S.kfin[pidx];
+      const int dk = kcur - S.kpart[pidx];
+      const bool pstart = live && i0 == pidx * pz;
+      const uint32_t cnt = live ? (uint32_t)(kChunk - (head ? o : 0)) : 0u;
+      const uint32_t tot = live ? (dk < 0 ? fs[0] : dk == 0 ? fs[1] : fs[2]) + cnt * (uint32_t)(kcur + 1) +
+                                      (pstart ? (uint32_t)pb : 0u)
+                                : 0u;
+      const uint32_t inc = wave_incl_scan32(tot);
+      if (lane == 63) S.scan[wv] = inc;
+      __syncthreads();
+      uint32_t p = pos + inc - tot;
+      for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
+      if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
+      const uint32_t kmask = (1u << kcur) - 1u;
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++) {
+        if (live && !(jj < 12 && head && jj < o)) {
+          const uint32_t qv = uu[jj] >> kcur;
+          lds_put(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
+          p += qv + 1u + (uint32_t)kcur;
+        }
+      }
+    } else {
     uint32_t kk[kChunk];  // Rice parameter | partition-start << 8, 0xFFFF = no code
     uint32_t tot = 0;
     int pidx = i0 < n ? i0 / pz : 0, pend = (pidx + 1) * pz;
@@ -665,6 +747,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
         lds_put(buf, p + qv, (k == 0) ? 1u : ((1u << k) | (uu[jj] & ((1u << k) - 1u))), k + 1);
         p += qv + 1u + (uint32_t)k;
       }
+    }
     }
   }
   __syncthreads();
