@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   {
     const NormParams np = norm_params(st, a.norm[fr.stream]);
-    load_channel(src, a.raster, st, fr, c, np, S.smp, orv, vmin, vmax);
+    const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
+    load_channel(src, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
   }
   orv = wave_or32(orv);
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys

@@ -29,6 +29,7 @@ namespace fra {
 hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, int vec_bytes, int rows, int max_rows,
                          hipStream_t s);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
+hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
@@ -90,6 +91,7 @@ struct fra_plan {
   size_t scan_tmp_bytes = 0;
   uint16_t* d_crctab = nullptr;
   uint32_t* d_tmp = nullptr;
+  int32_t* d_lut = nullptr;
   int64_t tmp_stride = 0;
   JobArgs args{};
   // timing
@@ -238,6 +240,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_scan_tmp);
   (void)hipFree(p->d_crctab);
   (void)hipFree(p->d_tmp);
+  (void)hipFree(p->d_lut);
   for (auto& e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;
@@ -362,6 +365,13 @@ static int plan_build(fra_plan* p) {
     HIPCHK(hipMalloc(&p->d_crctab, sizeof(uint16_t) * ct.size()));
     HIPCHK(hipMemcpy(p->d_crctab, ct.data(), sizeof(uint16_t) * ct.size(), hipMemcpyHostToDevice));
   }
+  // normalisation tables for <= 16-bit integer rasters (k_norm_lut -> gathered by k_analyze)
+  int64_t lut_stride = 0;
+  if (j.norm != 0 && (j.dtype == FRA_U8 || j.dtype == FRA_I8 || j.dtype == FRA_U16 || j.dtype == FRA_I16) &&
+      !p->streams.empty()) {
+    lut_stride = elem_size(j.dtype) == 1 ? 256 : 65536;
+    HIPCHK(hipMalloc(&p->d_lut, sizeof(int32_t) * (size_t)lut_stride * p->streams.size()));
+  }
   JobArgs& a = p->args;
   a.streams = p->d_streams;
   a.frames = p->d_frames;
@@ -374,6 +384,8 @@ static int plan_build(fra_plan* p) {
   a.crctab = p->d_crctab;
   a.tmp = p->d_tmp;
   a.tmp_stride = p->tmp_stride;
+  a.lut = p->d_lut;
+  a.lut_stride = lut_stride;
   a.nframes_total = nfr;
   a.cmax = p->cmax;
   a.blocksize = j.blocksize;
@@ -458,6 +470,7 @@ int fra_plan_execute(fra_plan* p) {
     const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
     HIPCHK(launch_minmax(p->src, a, nstreams, p->max_segs, vec, p->mm_rows, p->mm_max_rows, s));
     HIPCHK(launch_norm_finalize(a, nstreams, s));
+    HIPCHK(launch_norm_lut(p->src, a, nstreams, s));
   }
   if (p->timing) HIPCHK(hipEventRecord(p->ev[1], s));
   if (a.nframes_total > 0) HIPCHK(launch_analyze(p->src, p->b32, a, s));

@@ -108,8 +108,8 @@ template <> struct RawType<ST_F32> { using T = float; };
 // incrementally (no per-sample division or 64-bit multiply).  Returns per-thread OR / min / max.
 template <int SRC>
 __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                               const NormParams& np, int32_t* smp, uint32_t& orv, int32_t& vmin,
-                                               int32_t& vmax) {
+                                               const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
+                                               int32_t& vmin, int32_t& vmax) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
   const T* src = (const T*)base;
@@ -142,6 +142,25 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       }
     }
   }
+  if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
+    if (lut) {  // <= 16-bit integers: the normalised sample of value mn + d is lut[d] (k_norm_lut)
+      const int mnint = (int)np.mn;
+      int32_t v[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) v[k] = lut[(int)raw[k] - mnint];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const int i = t + k * kThreads;
+        if (i < n) {
+          smp[sidx(i)] = v[k];
+          orv |= (uint32_t)v[k];
+          vmin = min(vmin, v[k]);
+          vmax = max(vmax, v[k]);
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int i = t + k * kThreads;
@@ -157,17 +176,17 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
   }
 }
 __device__ __forceinline__ void load_channel(int src, const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                             const NormParams& np, int32_t* smp, uint32_t& orv, int32_t& vmin,
-                                             int32_t& vmax) {
+                                             const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
+                                             int32_t& vmin, int32_t& vmax) {
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_channel_t<ST_U8>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_I8: load_channel_t<ST_I8>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_U16: load_channel_t<ST_U16>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_I16: load_channel_t<ST_I16>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_U32: load_channel_t<ST_U32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_I32: load_channel_t<ST_I32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    case ST_F32: load_channel_t<ST_F32>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
-    default: load_channel_t<ST_F64>(base, st, fr, c, np, smp, orv, vmin, vmax); break;
+    case ST_U8: load_channel_t<ST_U8>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I8: load_channel_t<ST_I8>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U16: load_channel_t<ST_U16>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I16: load_channel_t<ST_I16>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U32: load_channel_t<ST_U32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I32: load_channel_t<ST_I32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_F32: load_channel_t<ST_F32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    default: load_channel_t<ST_F64>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
   }
 }
 

@@ -177,6 +177,8 @@ struct JobArgs {
   uint8_t* out;            // concatenated frames
   const uint16_t* crctab;  // CRC-16 slice-by-4 tables [4][256] + multiply-by-x^(8*2^i) tables [24][2][256]
   uint32_t* tmp;           // encoded subframes: slot (frame*cmax + channel) of tmp_stride words
+  const int32_t* lut;      // normalize_to_audio table per stream (<= 16-bit integer dtypes), or null
+  int64_t lut_stride;      // entries per stream: 256 (8-bit) or 65536 (16-bit); entry d = sample of mn + d
   int64_t tmp_stride;
   int32_t nframes_total;
   int32_t cmax;

@@ -188,6 +188,34 @@ __global__ void k_norm_finalize(const StreamDev* streams, NormDev* nd, int nstre
   nd[i].range = p.range;
 }
 
+// normalize_to_audio table of a <= 16-bit integer stream: entry d = the normalised sample of the raster
+// value mn + d, d = 0..mx-mn, by the same op sequence as norm_sample (k_analyze then gathers instead of
+// evaluating the float64 map per sample).  grid (64, streams), grid-stride over d.
+template <int SRC>
+__global__ void __launch_bounds__(256) k_norm_lut(const StreamDev* streams, const NormDev* nd, int32_t* lut,
+                                                  int64_t stride) {
+  const StreamDev st = streams[blockIdx.y];
+  if (st.norm == 0 || nd[blockIdx.y].mnkey == ~0ull) return;
+  const NormParams np = norm_params(st, nd[blockIdx.y]);
+  const int64_t R = (int64_t)np.range;  // integer data: mx - mn, or 1 for a constant stream
+  int32_t* out = lut + (int64_t)blockIdx.y * stride;
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d <= R && d < stride; d += (int64_t)gridDim.x * 256)
+    out[d] = norm_sample<SRC>(np.mn + (double)d, np);
+}
+
+hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s) {
+  if (!a.lut) return hipSuccess;
+  dim3 grid(64, (unsigned)nstreams);
+  switch (src) {
+    case ST_U8: k_norm_lut<ST_U8><<<grid, 256, 0, s>>>(a.streams, a.norm, (int32_t*)a.lut, a.lut_stride); break;
+    case ST_I8: k_norm_lut<ST_I8><<<grid, 256, 0, s>>>(a.streams, a.norm, (int32_t*)a.lut, a.lut_stride); break;
+    case ST_U16: k_norm_lut<ST_U16><<<grid, 256, 0, s>>>(a.streams, a.norm, (int32_t*)a.lut, a.lut_stride); break;
+    case ST_I16: k_norm_lut<ST_I16><<<grid, 256, 0, s>>>(a.streams, a.norm, (int32_t*)a.lut, a.lut_stride); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s) {
   k_norm_finalize<<<(nstreams + 255) / 256, 256, 0, s>>>(a.streams, a.norm, nstreams);
   return hipGetLastError();
