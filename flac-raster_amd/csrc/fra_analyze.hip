@@ -217,6 +217,8 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
     load_channel(src, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
   }
+  // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
+  for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
   orv = wave_or32(orv);
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys
   const uint32_t kmax = ~wave_min32(~((uint32_t)vmax ^ 0x80000000u));
@@ -333,13 +335,12 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 #pragma unroll
             for (int j = 1; j < MAXLAG; j++)
               if (lane == j + 1) e = errv[j];
-            const double bits = (lane >= 1 && lane <= nord) ? order_bits(e, n, lane, prec + sbps) : 0.0;
-            double best = __shfl(bits, 1, 64);
-            o = 1;
-            for (int oo = 2; oo <= nord; oo++) {
-              const double v = __shfl(bits, oo, 64);
-              if (v < best) { best = v; o = oo; }
-            }
+            // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as
+            // an unsigned integer; DPP min over the wave, lowest lane among the equal ones
+            const bool on = lane >= 1 && lane <= nord;
+            const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lane, prec + sbps)) : ~0ull;
+            const uint64_t kmin = wave_min64(key);
+            o = (int)__builtin_ctzll(__ballot(on && key == kmin));
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's lp rows -> all lanes
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
@@ -363,8 +364,6 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   // ---- 4. residual partition sums at the finest level P for every valid model (3.8)
   const int P = max_porder(n, 0, cfg.max_porder);
   const int psz = n >> P;
-  for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
-  __syncthreads();
   // x[j] = sample i0 - 12 + j: the last 12 of the previous chunk (the zero chunk for thread 0) and
   // this thread's 16 (samples past n are never counted: their sums/codes are masked by i0 < n / i < n)
   int32_t x[12 + kChunk];
@@ -376,6 +375,31 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   const bool head = i0 == 0;                    // this thread holds the warm-up samples (order <= 12 < 16)
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
+  if (!B32 && fastframe) {
+    // FIXED 0..4 by finite differences, in place, BEFORE the barrier that publishes wave 0's LPC
+    // models (waves 1-3 would otherwise idle there): after step k, x[j] for j >= 8 + k holds the
+    // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
+    // oracle's closed forms; every fixed model is valid here (n >= 16).
+#pragma unroll
+    for (int k = 0; k <= 4; k++) {
+      if (k > 0) {
+#pragma unroll
+        for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+      }
+      // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
+      uint32_t s32 = 0;
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
+      if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
+    }
+    if (MAXLAG > 0 && nmod > 5) {  // restore the samples for the LPC sums
+#pragma unroll
+      for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+    }
+  }
+  __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
   if (fastframe) {
     if constexpr (B32) {
       // 32-bps: FIXED k as the 4-tap integer predictor (int64), one model at a time
@@ -417,23 +441,6 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
       if constexpr (B32) {
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
-      }
-    }
-    if constexpr (!B32) {
-      // FIXED 0..4 by finite differences, in place (x is dead afterwards): after step k, x[j] for
-      // j >= 8 + k holds the k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.
-      // Same integers as the oracle's closed forms; every fixed model is valid here (n >= 16).
-#pragma unroll
-      for (int k = 0; k <= 4; k++) {
-        if (k > 0) {
-#pragma unroll
-          for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
-        }
-        // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
-        uint32_t s32 = 0;
-#pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
-        if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
       }
     }
   } else {

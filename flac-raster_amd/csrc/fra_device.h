@@ -243,6 +243,22 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t v) {  // wave-uniform re
   v = min(v, dpp32<DPP_BC31, 0xC>(v, ~0u));
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp64_old(uint64_t v, uint64_t old) {
+  const uint32_t lo = dpp32<CTRL, RM>((uint32_t)v, (uint32_t)old), hi = dpp32<CTRL, RM>((uint32_t)(v >> 32), (uint32_t)(old >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {  // wave-uniform result
+  v = min(v, dpp64_old<DPP_SHR1, 0xF>(v, ~0ull));
+  v = min(v, dpp64_old<DPP_SHR2, 0xF>(v, ~0ull));
+  v = min(v, dpp64_old<DPP_SHR4, 0xF>(v, ~0ull));
+  v = min(v, dpp64_old<DPP_SHR8, 0xF>(v, ~0ull));
+  v = min(v, dpp64_old<DPP_BC15, 0xA>(v, ~0ull));
+  v = min(v, dpp64_old<DPP_BC31, 0xC>(v, ~0ull));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
   v |= dpp32<DPP_SHR1, 0xF>(v);
   v |= dpp32<DPP_SHR2, 0xF>(v);
