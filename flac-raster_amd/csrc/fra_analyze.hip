@@ -217,6 +217,14 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
     load_channel(src, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
   }
+  // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window:
+  // issued here so their latency hides under the reductions and the barrier below
+  float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
+  if constexpr (MAXLAG > 0) {
+    const float* win = a.win + (size_t)fr.win * a.nwin * a.blocksize;
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[t * kChunk + j];  // table padded by kMaxLpc
+  }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
   orv = wave_or32(orv);
@@ -279,13 +287,18 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
       for (int wi = 0; wi < a.nwin; wi++) {
-        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+        if (wi > 0) {  // window 0 was prefetched during phase 1
+          const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+#pragma unroll
+          for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[i0 + j];  // table padded by kMaxLpc
+        }
         float wf[kChunk + MAXLAG];
 #pragma unroll
         for (int j = 0; j < kChunk + MAXLAG; j++) {
           const int i = i0 + j;
-          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * win[i] : 0.0f;
+          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * wcur[j] : 0.0f;
         }
+
         // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
         // float*float product, so this is bit-identical to the oracle's acc + a*b
         double acc[MAXLAG + 1];

@@ -345,11 +345,11 @@ static int plan_build(fra_plan* p) {
   HIPCHK(hipMalloc(&p->d_foff, sizeof(unsigned long long) * (nfr + 1)));
   HIPCHK(hipMalloc(&p->d_out, p->out_cap));
   const size_t wn = (size_t)std::max<size_t>(1, win_sizes.size()) * std::max(1, p->nwin) * j.blocksize;
-  std::vector<float> wt(wn, 0.0f);
+  std::vector<float> wt(wn + kMaxLpc, 0.0f);  // + lookahead pad: k_analyze reads win[i0 + j], j < 16 + max lag
   for (size_t t = 0; t < win_sizes.size(); t++)
     window_set(wt.data() + t * std::max(1, p->nwin) * j.blocksize, win_sizes[t], j.blocksize, nsub);
-  HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wn));
-  HIPCHK(hipMemcpy(p->d_win, wt.data(), sizeof(float) * wn, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wt.size()));
+  HIPCHK(hipMemcpy(p->d_win, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
   if (!p->streams.empty())
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
   if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
