@@ -320,11 +320,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
               if (i0 + jj + l < n) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
           }
         }
-#pragma unroll
-        for (int l = 0; l <= MAXLAG; l++) {
-          const double v = tree64(acc[l]);
-          if (lane == 63) S.red[wi & 1][wv][l] = v;
-        }
+        autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi & 1][wv], lane);
         __syncthreads();
         // wave 0, uniformly: autocorrelation -> Levinson-Durbin (registers) -> expected bits of every
         // order in parallel (lane o) -> first minimum -> qlp quantisation.  The other waves run ahead

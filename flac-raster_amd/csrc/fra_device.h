@@ -225,6 +225,58 @@ __device__ __forceinline__ double tree64(double v) {
   v = v + dppf64<DPP_BC31, 0xC>(v);
   return v;
 }
+// FRA-1 autocorrelation: the wave's 64 chunk partials of every lag reduced by the descending-stride
+// tree (32, 16, 8, 4, 2, 1; oracle ora_autocorr), as a reduce-scatter: strides 32 and 16 pair TWO
+// lags per v_permlane32/16_swap + add (each lane keeps one of the two node sums), the in-row strides
+// run the remaining values through DPP row_shr (upper lane keeps the node).  Every node is the sum
+// of the same two child nodes as in the oracle (IEEE addition is commutative), so the result is
+// bit-identical.  Lag sums are stored to red[lag] by lanes 15/31/47/63.
+__device__ __forceinline__ void swap32_f64(double& x, double& y) {
+  const uint64_t a = (uint64_t)__double_as_longlong(x), b = (uint64_t)__double_as_longlong(y);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)a, (uint32_t)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(a >> 32), (uint32_t)(b >> 32), false, false);
+  x = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+  y = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ void swap16_f64(double& x, double& y) {
+  const uint64_t a = (uint64_t)__double_as_longlong(x), b = (uint64_t)__double_as_longlong(y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)a, (uint32_t)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(a >> 32), (uint32_t)(b >> 32), false, false);
+  x = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+  y = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+}
+template <int NL>
+__device__ __forceinline__ void autocorr_reduce_wave(const double (&acc)[NL], double* red, int lane) {
+  constexpr int N32 = (NL + 1) / 2, N16 = (N32 + 1) / 2;
+  double w[N32];
+#pragma unroll
+  for (int k = 0; k < N32; k++) {  // stride 32: lanes < 32 keep lag 2k, lanes >= 32 lag 2k+1
+    double x = acc[2 * k], y = (2 * k + 1 < NL) ? acc[2 * k + 1] : acc[2 * k];
+    swap32_f64(x, y);
+    w[k] = x + y;
+  }
+  double z[N16];
+#pragma unroll
+  for (int k = 0; k < N16; k++) {  // stride 16: row r keeps w[2k + (r & 1)] of half r >> 1
+    double x = w[2 * k], y = (2 * k + 1 < N32) ? w[2 * k + 1] : w[2 * k];
+    swap16_f64(x, y);
+    z[k] = x + y;
+  }
+#pragma unroll
+  for (int k = 0; k < N16; k++) {  // strides 8, 4, 2, 1 inside the row: node at lane 15 of the row
+    double v = z[k];
+    v = v + dppf64<DPP_SHR8, 0xF>(v);
+    v = v + dppf64<DPP_SHR4, 0xF>(v);
+    v = v + dppf64<DPP_SHR2, 0xF>(v);
+    v = v + dppf64<DPP_SHR1, 0xF>(v);
+    if ((lane & 15) == 15) {
+      const int r = lane >> 4;
+      const int wi = (2 * k + 1 < N32) ? 2 * k + (r & 1) : 2 * k;
+      const int lag = (2 * wi + 1 < NL) ? 2 * wi + (r >> 1) : 2 * wi;
+      red[lag] = v;
+    }
+  }
+}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {  // wave-uniform result
   v += dpp32<DPP_SHR1, 0xF>(v);
   v += dpp32<DPP_SHR2, 0xF>(v);

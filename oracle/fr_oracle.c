@@ -234,7 +234,9 @@ ORA_API void ora_window_set(float *w /* nwin*N */, int N, int nsub) {
 
 /* Autocorrelation, FRA-1 fixed reduction order: 16-sample chunks summed sequentially
  * (acc starts at +0.0, products of two floats are exact in double), 256 chunk partials
- * (zero padded) reduced by a pairwise tree: stride 1,2,4,...,128, P[j] = P[j] + P[j+s]. */
+ * (zero padded); each group of 64 (one GPU wave) reduced by a pairwise tree with DESCENDING
+ * strides 32,16,...,1 (P[j] = P[j] + P[j+s], j < s inside the group), then the four group
+ * sums as (G0 + G1) + (G2 + G3). */
 ORA_API void ora_autocorr(const float *wf, int n, int maxlag, double *autoc) {
   double P[256];
   for (int l = 0; l <= maxlag; l++) {
@@ -245,9 +247,10 @@ ORA_API void ora_autocorr(const float *wf, int n, int maxlag, double *autoc) {
       }
       P[j] = acc;
     }
-    for (int s = 1; s < 256; s <<= 1)
-      for (int j = 0; j < 256; j += 2 * s) P[j] = P[j] + P[j + s];
-    autoc[l] = P[0];
+    for (int g = 0; g < 256; g += 64)
+      for (int s = 32; s >= 1; s >>= 1)
+        for (int j = g; j < g + s; j++) P[j] = P[j] + P[j + s];
+    autoc[l] = (P[0] + P[64]) + (P[128] + P[192]);
   }
 }
 
