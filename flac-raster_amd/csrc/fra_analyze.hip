@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   {
     const NormParams np = norm_params(st, a.norm[fr.stream]);
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
-    load_channel(src, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
+    load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
   }
   // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window:
   // issued here so their latency hides under the reductions and the barrier below

@@ -73,6 +73,7 @@ struct fra_plan {
   int nwin = 0;
   int max_segs = 0;
   int mm_vec = 0, mm_rows = 1, mm_max_rows = 0;  // vectorised k_minmax shape (0 = scalar path)
+  bool ld_vec8 = false;  // k_analyze 8-byte sample vectors possible (pointer alignment checked at execute)
   int cmax = 1;
   size_t raster_bytes = 0;
   // device buffers
@@ -332,6 +333,17 @@ static int plan_build(fra_plan* p) {
       break;
     }
   }
+  // k_analyze 8-byte sample vectors: V = 8/itemsize samples never straddle a row and stay aligned
+  {
+    const int64_t V = 8 / std::max(1, elem_size(j.dtype));
+    bool ok = elem_size(j.dtype) <= 4 && j.col_stride == 1 && j.blocksize % V == 0 && j.row_stride % V == 0 &&
+              (j.channels == 1 || j.band_stride % V == 0);
+    for (int w = 0; ok && w < j.nwindows; w++) {
+      const StreamDev& st = p->streams[w];
+      if (st.nsamples) ok = st.base_off % V == 0 && st.width % V == 0;
+    }
+    p->ld_vec8 = ok;
+  }
   if (nf_total > INT32_MAX / 2) return set_err(FRA_E_INVALID, "too many frames (%lld)", (long long)nf_total);
   p->raster_bytes = (size_t)max_extent * elem_size(j.dtype);
   p->out_cap = out_cap + 64;
@@ -463,6 +475,7 @@ int fra_plan_execute(fra_plan* p) {
   (void)hipSetDevice(p->ctx->device);
   hipStream_t s = p->ctx->stream;
   if (p->timing) collect_times(p);
+  p->args.vec8 = (p->ld_vec8 && (uintptr_t)p->d_raster % 8 == 0) ? 1 : 0;
   const JobArgs& a = p->args;
   const int nstreams = (int)p->streams.size();
   if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));

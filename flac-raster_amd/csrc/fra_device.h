@@ -103,17 +103,57 @@ template <> struct RawType<ST_U32> { using T = uint32_t; };
 template <> struct RawType<ST_I32> { using T = int32_t; };
 template <> struct RawType<ST_F32> { using T = float; };
 
-// Load channel c of frame fr into smp[0..n): lane-contiguous (coalesced) element reads; all of a
-// thread's 16 loads are issued before any is consumed (latency overlap), addresses advance
-// incrementally (no per-sample division or 64-bit multiply).  Returns per-thread OR / min / max.
-template <int SRC>
+template <typename T, int V>
+struct alignas(sizeof(T) * V) VecT {
+  T v[V];
+};
+
+// Load channel c of frame fr into smp[0..n): lane-contiguous (coalesced) reads; all of a thread's
+// loads are issued before any is consumed (latency overlap), addresses advance incrementally (no
+// per-sample division or 64-bit multiply).  VEC: 8-byte vectors of V = 8/itemsize samples (the
+// host checked that no vector straddles a row and all are aligned: JobArgs::vec8), thread t owns
+// vectors t + 256k; otherwise one element per lane, samples t + 256k.  Returns per-thread OR/min/max.
+template <int SRC, bool VEC>
 __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
                                                const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
                                                int32_t& vmin, int32_t& vmax) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
+  constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
   const T* src = (const T*)base;
   const int n = fr.n, w = st.width, t = threadIdx.x;
+  // sample index of raw[k]
+  auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
+  T raw[K];
+  if constexpr (VEC) {
+    using VT = VecT<T, V>;
+    int col = fr.col0 + t * V, row = fr.row0;
+    if (col >= w) {
+      const int q = (int)((unsigned)col / (unsigned)w);
+      row += q;
+      col -= q * w;
+    }
+    int64_t e = st.base_off + (int64_t)c * st.band_stride + (int64_t)row * st.row_stride + col;
+    const int step = kThreads * V;
+    const int64_t wrap = st.row_stride - (int64_t)w;
+    const int64_t e_first = st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride + fr.col0;
+#pragma unroll
+    for (int kv = 0; kv < K / V; kv++) {
+      const VT x = *(const VT*)(src + (((t + kv * kThreads) * V < n) ? e : e_first));
+#pragma unroll
+      for (int ee = 0; ee < V; ee++) raw[kv * V + ee] = x.v[ee];
+      col += step;
+      e += step;
+      if (col >= w) {
+        if (w >= step) { col -= w; e += wrap; }
+        else {
+          const int q = (int)((unsigned)col / (unsigned)w);
+          col -= q * w;
+          e += (int64_t)q * wrap;
+        }
+      }
+    }
+  } else {
   int col = fr.col0 + t, row = fr.row0;
   if (col >= w) {
     const int q = (int)((unsigned)col / (unsigned)w);
@@ -127,7 +167,6 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
   // unconditional and the compiler can keep all K in flight
   const int64_t e_first = st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride +
                           (int64_t)fr.col0 * st.col_stride;
-  T raw[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     raw[k] = src[(t + k * kThreads < n) ? e : e_first];
@@ -142,6 +181,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       }
     }
   }
+  }
   if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
     if (lut) {  // <= 16-bit integers: the normalised sample of value mn + d is lut[d] (k_norm_lut)
       const int mnint = (int)np.mn;
@@ -150,7 +190,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       for (int k = 0; k < K; k++) v[k] = lut[(int)raw[k] - mnint];
 #pragma unroll
       for (int k = 0; k < K; k++) {
-        const int i = t + k * kThreads;
+        const int i = sidx_of(k);
         if (i < n) {
           smp[sidx(i)] = v[k];
           orv |= (uint32_t)v[k];
@@ -163,7 +203,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
   }
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const int i = t + k * kThreads;
+    const int i = sidx_of(k);
     if (i < n) {
       int32_t v;
       if (np.mode == 0) v = (int32_t)raw[k];
@@ -175,18 +215,30 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
     }
   }
 }
-__device__ __forceinline__ void load_channel(int src, const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                             const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
-                                             int32_t& vmin, int32_t& vmax) {
+__device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const StreamDev& st, const FrameDev& fr,
+                                             int c, const NormParams& np, const int32_t* lut, int32_t* smp,
+                                             uint32_t& orv, int32_t& vmin, int32_t& vmax) {
+  if (vec8) {
+    switch (src) {  // wave-uniform dispatch; f64 never takes the vector path
+      case ST_U8: load_channel_t<ST_U8, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I8: load_channel_t<ST_I8, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U16: load_channel_t<ST_U16, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I16: load_channel_t<ST_I16, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U32: load_channel_t<ST_U32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I32: load_channel_t<ST_I32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_F32: load_channel_t<ST_F32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      default: break;
+    }
+  }
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_channel_t<ST_U8>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I8: load_channel_t<ST_I8>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U16: load_channel_t<ST_U16>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I16: load_channel_t<ST_I16>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U32: load_channel_t<ST_U32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I32: load_channel_t<ST_I32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_F32: load_channel_t<ST_F32>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    default: load_channel_t<ST_F64>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U8: load_channel_t<ST_U8, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I8: load_channel_t<ST_I8, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U16: load_channel_t<ST_U16, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I16: load_channel_t<ST_I16, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U32: load_channel_t<ST_U32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I32: load_channel_t<ST_I32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_F32: load_channel_t<ST_F32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    default: load_channel_t<ST_F64, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
   }
 }
 

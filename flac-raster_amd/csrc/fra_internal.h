@@ -185,6 +185,7 @@ struct JobArgs {
   int32_t blocksize;
   int32_t level;
   int32_t nwin;
+  int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
 };
 
 }  // namespace fra

@@ -88,10 +88,6 @@ __global__ void __launch_bounds__(256) k_minmax(const void* raster, const Stream
 // per thread.  Per element: a 32-bit ordered key (integers: value / sign-flipped, f32: IEEE order
 // key, NaN skipped) -- the same total order as okey() on the float64 value, so the result equals
 // k_minmax's.
-template <typename T, int V>
-struct alignas(sizeof(T) * V) VecT {
-  T v[V];
-};
 template <int SRC>
 __device__ __forceinline__ uint32_t key32(typename RawType<SRC>::T x, bool& ok) {
   if constexpr (SRC == ST_U8 || SRC == ST_U16 || SRC == ST_U32) {
