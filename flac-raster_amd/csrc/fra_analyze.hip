@@ -281,8 +281,43 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     }
   }
 
-  // ---- 3. LPC analysis per apodization window (3.4-3.7)
+  // ---- 3a. partition geometry; FIXED residual sums of the fast 16-bit path (3.8), before the LPC
+  // analysis: their partition search then runs on waves 1-3 while wave 0 does Levinson-Durbin
+  const int P = max_porder(n, 0, cfg.max_porder);
+  const int psz = n >> P;
+  // x[j] = sample i0 - 12 + j: the last 12 of the previous chunk (the zero chunk for thread 0) and
+  // this thread's 16 (samples past n are never counted: their sums/codes are masked by i0 < n / i < n)
+  int32_t x[12 + kChunk];
+  const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
+  const bool head = i0 == 0;                    // this thread holds the warm-up samples (order <= 12 < 16)
+  const int pidx0 = i0 < n ? i0 / psz : 0;
+  const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
+  if (!B32 && fastframe) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+#pragma unroll
+    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+    // FIXED 0..4 by finite differences, in place: after step k, x[j] for j >= 8 + k holds the
+    // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
+    // oracle's closed forms; every fixed model is valid here (n >= 16).
+#pragma unroll
+    for (int k = 0; k <= 4; k++) {
+      if (k > 0) {
+#pragma unroll
+        for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+      }
+      // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
+      uint32_t s32 = 0;
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
+      if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
+    }
+  }
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
+  // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
+  const bool early = !B32 && fastframe && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
+
+  // ---- 3. LPC analysis per apodization window (3.4-3.7)
   const int prec = qlp_precision(bps, n);
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
@@ -322,6 +357,18 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
         }
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi & 1][wv], lane);
         __syncthreads();
+        if (early && wi == 0 && wv != 0) {  // FIXED 0..4 over waves 1-3 while wave 0 runs the LD below
+          for (int m = wv - 1; m < 5; m += 3) {
+            const int pm = max_porder(n, m, cfg.max_porder);
+            uint64_t best = 0;
+            int bp = pm;
+            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
+            if (lane == 0) {
+              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
+              S.mporder[m] = bp;
+            }
+          }
+        }
         // wave 0, uniformly: autocorrelation -> Levinson-Durbin (registers) -> expected bits of every
         // order in parallel (lane o) -> first minimum -> qlp quantisation.  The other waves run ahead
         // (next window / model-sum setup); red[] is double-buffered and the next barrier is only
@@ -371,42 +418,11 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 
   FRA_STOP(2)
   // ---- 4. residual partition sums at the finest level P for every valid model (3.8)
-  const int P = max_porder(n, 0, cfg.max_porder);
-  const int psz = n >> P;
-  // x[j] = sample i0 - 12 + j: the last 12 of the previous chunk (the zero chunk for thread 0) and
-  // this thread's 16 (samples past n are never counted: their sums/codes are masked by i0 < n / i < n)
-  int32_t x[12 + kChunk];
+  {  // (the fast 16-bit path's FIXED sums consumed x)
 #pragma unroll
-  for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
 #pragma unroll
-  for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
-  const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
-  const bool head = i0 == 0;                    // this thread holds the warm-up samples (order <= 12 < 16)
-  const int pidx0 = i0 < n ? i0 / psz : 0;
-  const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
-  if (!B32 && fastframe) {
-    // FIXED 0..4 by finite differences, in place, BEFORE the barrier that publishes wave 0's LPC
-    // models (waves 1-3 would otherwise idle there): after step k, x[j] for j >= 8 + k holds the
-    // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
-    // oracle's closed forms; every fixed model is valid here (n >= 16).
-#pragma unroll
-    for (int k = 0; k <= 4; k++) {
-      if (k > 0) {
-#pragma unroll
-        for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
-      }
-      // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
-      uint32_t s32 = 0;
-#pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
-      if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
-    }
-    if (MAXLAG > 0 && nmod > 5) {  // restore the samples for the LPC sums
-#pragma unroll
-      for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
-#pragma unroll
-      for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
-    }
+    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
   }
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
   if (fastframe) {
@@ -487,7 +503,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
 
   FRA_STOP(3)
   // ---- 5. every partition order of a model in one pass (one wave per model)
-  for (int m = wv; m < nmod; m += 4) {
+  for (int m = (early ? 5 : 0) + wv; m < nmod; m += 4) {
     if (!S.mvalid[m]) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
