@@ -61,9 +61,9 @@ template <bool B32>
 __device__ __forceinline__ void acc_zz(int64_t r, bool on, uint64_t& acc, bool& ovf) {
   if constexpr (B32) {
     ovf |= on && (r > INT32_MAX || r < INT32_MIN);
-    acc += on ? zz64(r) : 0ull;
+    acc += on ? abs2_64(r) : 0ull;
   } else {
-    acc += on ? zz32((int32_t)r) : 0u;  // |r| < 2^27: 16 values fit in 32 bits, widened once
+    acc += on ? abs2_64(r) : 0u;
   }
 }
 // FIXED orders 0..4 at once: the order-k residual is the k-th finite difference of the samples,
@@ -97,15 +97,39 @@ __device__ __forceinline__ uint64_t lpc_sum_fast(const int32_t* x, const int32_t
   return acc;
 }
 
-// 16-bit path: sum of zig-zag LPC residuals of the thread's 16 samples in 32 bits (|r| < 2^27, see
-// acc_zz); the warm-up positions jj < O are masked for thread 0 only (compile-time bound)
+// 16-bit path LPC predictor with v_dot2c_i32_i16: samples fit int16 and |q| < 2^11, so the pairwise
+// int16 products accumulate exactly in int32 (|sum| < 12 * 2^26); q pairs Q[p] = (q[2p], q[2p+1]),
+// sample pairs A(m) = (x[m], x[m-1]) -> pred(b) = sum_p dot2(A(b - 1 - 2p), Q[p])
+typedef short fra_short2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fra_short2 pack_pair(int32_t lo, int32_t hi) {
+  return __builtin_bit_cast(fra_short2, __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u));
+}
+template <int NP>
+__device__ __forceinline__ int32_t pred_dot2(const int32_t* x, int b, const fra_short2 (&Q)[NP]) {
+  int32_t acc = 0;
+#pragma unroll
+  for (int p = 0; p < NP; p++) acc = __builtin_amdgcn_sdot2(pack_pair(x[b - 1 - 2 * p], x[b - 2 - 2 * p]), Q[p], acc, false);
+  return acc;
+}
+template <int NP>
+__device__ __forceinline__ void q_pairs(const int32_t* q, fra_short2 (&Q)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; p++) Q[p] = pack_pair(q[2 * p], q[2 * p + 1]);
+}
+// 16-bit path: sum of |LPC residual| over the thread's 16 samples (|r| < 2^27: fits 32 bits), warm-up
+// positions jj < O masked for thread 0 only (compile-time bound); the caller doubles it (3.8)
 template <int O>
-__device__ __forceinline__ uint64_t lpc_sum16(const int32_t* x, const int32_t* q, int sh, bool head) {
+__device__ __forceinline__ uint32_t lpc_abs16(const int32_t* x, const int32_t* q, int sh, bool head) {
+  constexpr int NP = (O + 1) / 2;
+  fra_short2 Q[NP];
+  q_pairs<NP>(q, Q);
   uint32_t acc = 0;
 #pragma unroll
   for (int jj = 0; jj < kChunk; jj++) {
-    const uint32_t u = zz32((int32_t)gres<false, O>(x, jj, q, sh));
-    acc += (jj < O && head) ? 0u : u;
+    const int b = 12 + jj;
+    const uint32_t xb = (uint32_t)x[b] ^ kBias;
+    const uint32_t pb = (uint32_t)(pred_dot2<NP>(x, b, Q) >> sh) ^ kBias;
+    acc = sad_acc(xb, (jj < O && head) ? xb : pb, acc);
   }
   return acc;
 }
@@ -300,17 +324,23 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     // FIXED 0..4 by finite differences, in place: after step k, x[j] for j >= 8 + k holds the
     // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
     // oracle's closed forms; every fixed model is valid here (n >= 16).
+    // order k residual at j = the (k-1)-th difference x[j] - x[j-1]; |.| by v_sad_u32 on biased values
+    // (x holds the (k-1)-th difference for j >= 7 + k); warm-up samples 0..k-1 belong to thread 0
+    // (i0 == 0): those k positions compare a value with itself
 #pragma unroll
     for (int k = 0; k <= 4; k++) {
-      if (k > 0) {
+      if (k > 1) {
 #pragma unroll
-        for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+        for (int j = 12 + kChunk - 1; j >= 7 + k; j--) x[j] = x[j] - x[j - 1];
       }
-      // warm-up samples 0..k-1 belong to thread 0 (i0 == 0): only those k positions are masked
       uint32_t s32 = 0;
 #pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) s32 += (jj < k && head) ? 0u : zz32(x[12 + jj]);
-      if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], (unsigned long long)s32);
+      for (int jj = 0; jj < kChunk; jj++) {
+        const uint32_t ab = (uint32_t)x[12 + jj] ^ kBias;
+        const uint32_t bb = k == 0 ? kBias : ((jj < k && head) ? ab : (uint32_t)x[11 + jj] ^ kBias);
+        s32 = sad_acc(ab, bb, s32);
+      }
+      if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], 2ull * s32);
     }
   }
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
@@ -456,7 +486,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   case O_:           \
     if constexpr (O_ <= MAXO) { \
       if constexpr (B32) acc = lpc_sum_fast<B32, O_>(x, q, sh, skip, ovf); \
-      else acc = lpc_sum16<O_>(x, q, sh, head); \
+      else acc = 2ull * lpc_abs16<O_>(x, q, sh, head); \
     } \
     break;
         FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6)
@@ -490,7 +520,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
           }
           const int64_t r = gres_lds<B32, MAXO>(S.smp, i, q, sh);
           if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
-          acc += zz64(r);
+          acc += abs2_64(r);
         }
         if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
       }
@@ -577,7 +607,12 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++)
-        uu[jj] = B32 ? (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh)) : zz32((int32_t)gres<B32, MAXO>(x, jj, q, sh));
+        if constexpr (B32) uu[jj] = (uint32_t)zz64(gres<B32, MAXO>(x, jj, q, sh));
+        else {
+          fra_short2 Q[(MAXO + 1) / 2];
+          q_pairs<(MAXO + 1) / 2>(q, Q);
+          uu[jj] = zz32(x[12 + jj] - (pred_dot2<(MAXO + 1) / 2>(x, 12 + jj, Q) >> sh));
+        }
     }
     if (head) {
 #pragma unroll

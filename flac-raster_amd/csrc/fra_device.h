@@ -389,6 +389,13 @@ __device__ __forceinline__ uint64_t zz64(int64_t r) {
   return r >= 0 ? ((uint64_t)r << 1) : ((((uint64_t)(-(r + 1))) << 1) | 1u);
 }
 __device__ __forceinline__ uint32_t zz32(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
+// |a - b| + acc for int32 a, b given as a ^ 2^31, b ^ 2^31 (unsigned order == signed order): one
+// v_sad_u32.  The estimate sums are 2 * sum |r|.
+constexpr uint32_t kBias = 0x80000000u;
+__device__ __forceinline__ uint32_t sad_acc(uint32_t ab, uint32_t bb, uint32_t acc) {
+  return (ab > bb ? ab - bb : bb - ab) + acc;
+}
+__device__ __forceinline__ uint64_t abs2_64(int64_t r) { return 2 * (uint64_t)(r < 0 ? -r : r); }
 __device__ __forceinline__ int bitlen64(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
 
 // Rice parameter estimate == oracle rice_pick: kc = bitlen(S / n) computed without

@@ -422,7 +422,9 @@ static int compute_residual(const int64_t *s, int n, int type, int o, const int3
 }
 static inline uint64_t zz(int64_t r) { return r >= 0 ? (uint64_t)r << 1 : ((uint64_t)(-(r + 1)) << 1) | 1u; }
 
-/* Estimated residual bits for a model + best partition order (3.8). Fills porder & k[]. */
+/* Estimated residual bits for a model + best partition order (3.8). Fills porder & k[].
+ * The partition sums are S = sum of 2|r| (an upper bound of the zig-zag sum that differs by the
+ * count of negative residuals; the GPU forms |r| with one v_sad_u32 per residual). */
 static uint64_t residual_estimate(const int64_t *r, int n, int o, int pcap, int *porder_out, int *k_out) {
   int pmax = max_porder(n, o, pcap);
   uint64_t sums[256];
@@ -430,7 +432,7 @@ static uint64_t residual_estimate(const int64_t *r, int n, int o, int pcap, int 
   for (int j = 0; j < np; j++) {
     uint64_t S = 0;
     int a = j == 0 ? o : j * ps, b = (j + 1) * ps;
-    for (int i = a; i < b; i++) S += zz(r[i]);
+    for (int i = a; i < b; i++) S += 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
     sums[j] = S;
   }
   uint64_t best = 0;
