@@ -351,17 +351,16 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   const int prec = qlp_precision(bps, n);
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
-      for (int wi = 0; wi < a.nwin; wi++) {
-        if (wi > 0) {  // window 0 was prefetched during phase 1
-          const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
-#pragma unroll
-          for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[i0 + j];  // table padded by kMaxLpc
-        }
+      // one apodization window: windowed samples -> chunk partials -> wave reduce-scatter -> barrier ->
+      // (window 0: FIXED searches on waves 1-3) + wave 0's Levinson-Durbin / order / quantisation.
+      // Window 0 is peeled so its prefetched coefficients are dead after its first use (no live range
+      // across the Levinson-Durbin section, which otherwise spills).
+      auto window_pass = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG]) {
         float wf[kChunk + MAXLAG];
 #pragma unroll
         for (int j = 0; j < kChunk + MAXLAG; j++) {
           const int i = i0 + j;
-          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * wcur[j] : 0.0f;
+          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * wcoef[j] : 0.0f;
         }
 
         // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
@@ -442,6 +441,14 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
             for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
           }
         }
+      };
+      window_pass(0, wcur);
+      for (int wi = 1; wi < a.nwin; wi++) {
+        float wl[kChunk + MAXLAG];
+        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+#pragma unroll
+        for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
+        window_pass(wi, wl);
       }
     }
   }
