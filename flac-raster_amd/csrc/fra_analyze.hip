@@ -40,6 +40,7 @@ struct AnalyzeSmem {
     uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
   } u;
   unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
+  unsigned long long esum2[kMaxPart][3];     // fast frames: exact-pass sums of u >> (k0-1), u >> k0, u >> (k0+1)
   double red[2][4][kMaxLpc + 1];  // double-buffered by window parity
   double autoc[kMaxLpc + 1];
   double lp[kMaxLpc][kMaxLpc];
@@ -251,6 +252,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
+  for (int i = t; i < kMaxPart * 3; i += kThreads) (&S.esum2[0][0])[i] = 0ull;
   orv = wave_or32(orv);
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys
   const uint32_t kmax = ~wave_min32(~((uint32_t)vmax ^ 0x80000000u));
@@ -553,6 +555,175 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
     }
   }
   __syncthreads();
+  if constexpr (!B32) {
+    if (fastframe) {
+      // ---- 6+7, fast 16-bit frames: every wave derives the winner and the partition Rice parameters
+      // itself (same integers in every wave: no wave-0 section + broadcast barrier), exact sums by LDS
+      // atomics, the same refinement in every wave, then the encoder.  4 barriers instead of 7.
+      uint32_t key = ~0u;
+      if (lane < nmod && S.mvalid[lane]) key = (S.mest[lane] << 5) | (uint32_t)lane;
+      const int m = (int)(wave_min32(key) & 31u);
+      const int type = __builtin_amdgcn_readfirstlane(S.mtype[m]);
+      const int o = __builtin_amdgcn_readfirstlane(S.morder[m]);
+      const int sh = __builtin_amdgcn_readfirstlane(S.mshift[m]);
+      const int ps = __builtin_amdgcn_readfirstlane(S.mporder[m]);
+      // estimate k per partition of order ps: upper-lane sums of the finest sums (3.8), leader lane
+      // ((j+1) << smax) - 1 of partition j holds its k
+      const int smax = P - ps;
+      uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
+      if (smax > 0) Sv = up_add64<0>(Sv);
+      if (smax > 1) Sv = up_add64<1>(Sv);
+      if (smax > 2) Sv = up_add64<2>(Sv);
+      if (smax > 3) Sv = up_add64<3>(Sv);
+      if (smax > 4) Sv = up_add64<4>(Sv);
+      if (smax > 5) Sv = up_add64<5>(Sv);
+      int kl;
+      {
+        const int j = lane >> smax;
+        uint64_t bits;
+        rice_pick((uint64_t)((n >> ps) - (j == 0 ? o : 0)), Sv, kl, bits);
+      }
+      const int pz = n >> ps;
+      const bool live = i0 < n;
+      const int pidx = live ? i0 / pz : 0;
+      const int k0 = __shfl(kl, ((pidx + 1) << smax) - 1, 64);
+      // zig-zag residuals of the winner (exact code values), warm-up samples 0
+      uint32_t uu[kChunk];
+#pragma unroll
+      for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+      if (type == 2) {
+#pragma unroll
+        for (int k = 1; k <= 4; k++) {
+          if (k <= o) {
+#pragma unroll
+            for (int j = 12 + kChunk - 1; j >= 8 + k; j--) x[j] = x[j] - x[j - 1];
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj]);
+      } else {
+        int32_t q[MAXO];
+#pragma unroll
+        for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+        fra_short2 Q[(MAXO + 1) / 2];
+        q_pairs<(MAXO + 1) / 2>(q, Q);
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj] - (pred_dot2<(MAXO + 1) / 2>(x, 12 + jj, Q) >> sh));
+      }
+      if (head) {
+#pragma unroll
+        for (int jj = 0; jj < 12; jj++)
+          if (jj < o) uu[jj] = 0u;
+      }
+      uint32_t fs0 = 0, fs1 = 0, fs2 = 0;  // u < 2^28: 16 of them fit 32 bits
+      {
+        const int km = k0 > 0 ? k0 - 1 : 0;  // fs0 is only used when k0 >= 1
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) {
+          fs0 += uu[jj] >> km;
+          fs1 += uu[jj] >> k0;
+          fs2 += uu[jj] >> (k0 + 1);
+        }
+      }
+      if (live) {
+        atomicAdd(&S.esum2[pidx][0], (unsigned long long)fs0);
+        atomicAdd(&S.esum2[pidx][1], (unsigned long long)fs1);
+        atomicAdd(&S.esum2[pidx][2], (unsigned long long)fs2);
+      }
+      __syncthreads();
+      // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
+      const int npp = 1 << ps;
+      const int k0j = __shfl(kl, lane < npp ? ((lane + 1) << smax) - 1 : 0, 64);
+      uint64_t best = 0;
+      int bk = 0;
+      if (lane < npp) {
+        const uint64_t cnt = (uint64_t)(pz - (lane == 0 ? o : 0));
+        bool first = true;
+        for (int kk = k0j - 1; kk <= k0j + 1; kk++) {
+          if (kk < 0 || kk > 30) continue;
+          const uint64_t e = cnt * (uint64_t)(kk + 1) + S.esum2[lane][kk - k0j + 1];
+          if (first || e < best) { best = e; bk = kk; first = false; }
+        }
+      }
+      const bool big = __any(lane < npp && bk > 14);
+      const uint64_t rtot = (uint64_t)wave_sum32(lane < npp ? (uint32_t)best : 0u) + (uint64_t)npp * (big ? 5 : 4) + 6;
+      const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
+      const bool verbatim = exact >= verb;
+      const int kcur = __shfl(bk, pidx, 64);
+      if (wv == 0) {
+        if (lane < npp) d->k[lane] = (uint8_t)bk;
+        if (lane < kMaxLpc) d->coef[lane] = type == 3 ? S.mcoef[m][lane] : 0;
+        if (lane == 0) {
+          d->wasted = (uint8_t)w;
+          d->sbps = (uint8_t)sbps;
+          d->cval = 0;
+          if (verbatim) {
+            d->type = 1; d->order = 0; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
+            d->bits = verb;
+          } else {
+            d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
+            d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh;
+            d->bits = (uint32_t)exact;
+          }
+        }
+      }
+      // encode (RFC 9639 9.2) into the LDS bit buffer (over psum: every wave is past its psum reads)
+      const uint32_t fbits = verbatim ? verb : (uint32_t)exact;
+      const uint32_t nw = (fbits + 31) >> 5;
+      uint32_t* buf = S.u.buf;
+      for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
+      const int pb = big ? 5 : 4;
+      const int dk = kcur - k0;
+      const bool pstart = live && i0 == pidx * pz;
+      const uint32_t cnt = live ? (uint32_t)(kChunk - (head ? o : 0)) : 0u;
+      const uint32_t tot = (live && !verbatim)
+                               ? (dk < 0 ? fs0 : dk == 0 ? fs1 : fs2) + cnt * (uint32_t)(kcur + 1) + (pstart ? (uint32_t)pb : 0u)
+                               : 0u;
+      const uint32_t inc = wave_incl_scan32(tot);
+      if (lane == 63) S.scan[wv] = inc;
+      __syncthreads();
+      const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
+      if (t == 0) {
+        const int tcode = verbatim ? 1 : type == 2 ? 8 + o : 31 + o;
+        lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
+      }
+      if (verbatim) {
+        for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
+      } else {
+        if (t < o) lds_put(buf, hdr + (uint32_t)t * sbps, (uint32_t)S.smp[sidx(t)] & smask, sbps);
+        uint32_t pos = hdr + (uint32_t)o * sbps;
+        if (type == 3) {
+          if (t == 0) {
+            lds_put(buf, pos, (uint32_t)(prec - 1), 4);
+            lds_put(buf, pos + 4, (uint32_t)sh & 31u, 5);
+          }
+          if (t < o) lds_put(buf, pos + 9 + (uint32_t)t * prec, (uint32_t)S.mcoef[m][t] & ((1u << prec) - 1u), prec);
+          pos += 9 + (uint32_t)o * prec;
+        }
+        if (t == 0) lds_put(buf, pos, ((uint32_t)(big ? 1 : 0) << 4) | (uint32_t)ps, 6);
+        pos += 6;
+        uint32_t p = pos + inc - tot;
+        for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
+        if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
+        const uint32_t kmask = (1u << kcur) - 1u;
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) {
+          if (live && !(jj < 12 && head && jj < o)) {
+            const uint32_t qv = uu[jj] >> kcur;
+            lds_put(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
+            p += qv + 1u + (uint32_t)kcur;
+          }
+        }
+      }
+      __syncthreads();
+      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+      for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+      return;
+    }
+  }
   if (wv == 0) {  // winner = first minimal estimate: argmin over (estimate, model index)
     uint32_t key = ~0u;
     if (lane < nmod && S.mvalid[lane]) key = (S.mest[lane] << 5) | (uint32_t)lane;
