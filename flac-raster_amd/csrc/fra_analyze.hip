@@ -32,9 +32,60 @@ namespace fra {
 template <bool B32>
 constexpr int buf_words() { return B32 ? kMaxBlock + 16 : kMaxBlock / 2 + 16; }
 
+// per-thread sample windows from the LDS array (chunk stride kSmpStride elements):
+//   read_x28: x[j] = sample 16t - 12 + j (the previous chunk's last 12, the zero chunk for t = 0)
+//   read_y24: y[j] = sample 16t + j, j < 24 (this chunk + the next chunk's first 8)
+// int16 storage is read as aligned dword pairs and sign-extended (2 samples per ds_read lane-dword)
+__device__ __forceinline__ int32_t lo16(uint32_t v) { return (int32_t)(int16_t)(v & 0xFFFFu); }
+__device__ __forceinline__ int32_t hi16(uint32_t v) { return (int32_t)v >> 16; }
+__device__ __forceinline__ void read_x28(const int32_t* smp, int t, int32_t (&x)[28]) {
+#pragma unroll
+  for (int j = 0; j < 12; j++) x[j] = smp[t * kSmpStride + 4 + j];
+#pragma unroll
+  for (int j = 0; j < 16; j++) x[12 + j] = smp[(t + 1) * kSmpStride + j];
+}
+__device__ __forceinline__ void read_x28(const int16_t* smp, int t, int32_t (&x)[28]) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(smp);  // kSmpStride even: chunk starts dword-aligned
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const uint32_t v = d[(t * kSmpStride + 4) / 2 + j];
+    x[2 * j] = lo16(v);
+    x[2 * j + 1] = hi16(v);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t v = d[(t + 1) * kSmpStride / 2 + j];
+    x[12 + 2 * j] = lo16(v);
+    x[13 + 2 * j] = hi16(v);
+  }
+}
+__device__ __forceinline__ void read_y24(const int32_t* smp, int t, int32_t (&y)[24]) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) y[j] = smp[(t + 1) * kSmpStride + j];
+#pragma unroll
+  for (int j = 0; j < 8; j++) y[16 + j] = smp[(t + 2) * kSmpStride + j];
+}
+__device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)[24]) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(smp);
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t v = d[(t + 1) * kSmpStride / 2 + j];
+    y[2 * j] = lo16(v);
+    y[2 * j + 1] = hi16(v);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t v = d[(t + 2) * kSmpStride / 2 + j];
+    y[16 + 2 * j] = lo16(v);
+    y[17 + 2 * j] = hi16(v);
+  }
+}
+
 template <bool B32>
 struct AnalyzeSmem {
-  int32_t smp[kSmpWords];  // sample i at sidx(i); words [0, kSmpStride) = zero chunk
+  // sample i at sidx(i); [0, kSmpStride) = zero chunk.  16-bit path: int16 (every sample fits), which
+  // keeps the workgroup at <= 32 KiB LDS (5 workgroups per CU at 96 VGPRs)
+  typename std::conditional<B32, int32_t, int16_t>::type smp[kSmpWords];
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
     uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
@@ -211,7 +262,7 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
 }
 
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : 5) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32> S;
   const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -319,10 +370,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
   if (!B32 && fastframe) {
-#pragma unroll
-    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
-#pragma unroll
-    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+read_x28(S.smp, t, x);
     // FIXED 0..4 by finite differences, in place: after step k, x[j] for j >= 8 + k holds the
     // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
     // oracle's closed forms; every fixed model is valid here (n >= 16).
@@ -359,10 +407,15 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       // across the Levinson-Durbin section, which otherwise spills).
       auto window_pass = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG]) {
         float wf[kChunk + MAXLAG];
+        {
+          int32_t y[kChunk + 8];
+          read_y24(S.smp, t, y);
 #pragma unroll
-        for (int j = 0; j < kChunk + MAXLAG; j++) {
-          const int i = i0 + j;
-          wf[j] = (i < n) ? (float)S.smp[sidx(i)] * wcoef[j] : 0.0f;
+          for (int j = 0; j < kChunk + MAXLAG; j++) {
+            const int i = i0 + j;
+            const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
+            wf[j] = (i < n) ? (float)v * wcoef[j] : 0.0f;
+          }
         }
 
         // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
@@ -458,10 +511,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   FRA_STOP(2)
   // ---- 4. residual partition sums at the finest level P for every valid model (3.8)
   {  // (the fast 16-bit path's FIXED sums consumed x)
-#pragma unroll
-    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
-#pragma unroll
-    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+read_x28(S.smp, t, x);
   }
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
   if (fastframe) {
@@ -589,10 +639,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
       const int k0 = __shfl(kl, ((pidx + 1) << smax) - 1, 64);
       // zig-zag residuals of the winner (exact code values), warm-up samples 0
       uint32_t uu[kChunk];
-#pragma unroll
-      for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
-#pragma unroll
-      for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+read_x28(S.smp, t, x);
       if (type == 2) {
 #pragma unroll
         for (int k = 1; k <= 4; k++) {
@@ -764,10 +811,7 @@ __global__ void __launch_bounds__(kThreads, 4) k_analyze(JobArgs a, int src) {
   uint32_t fs[3] = {0u, 0u, 0u};  // fast frames: this thread's sums of u >> (k0-1), u >> k0, u >> (k0+1)
   if (fastframe) {
     // reload the sample window from LDS (keeps the phase-4 window registers dead across the search)
-#pragma unroll
-    for (int j = 0; j < 12; j++) x[j] = S.smp[t * kSmpStride + 4 + j];
-#pragma unroll
-    for (int j = 0; j < kChunk; j++) x[12 + j] = S.smp[(t + 1) * kSmpStride + j];
+read_x28(S.smp, t, x);
     if (!B32 && type == 2) {
       // FIXED winner: the o-th finite difference in place (wave-uniform o), as in phase 4
 #pragma unroll

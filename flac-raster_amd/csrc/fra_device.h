@@ -113,9 +113,9 @@ struct alignas(sizeof(T) * V) VecT {
 // per-sample division or 64-bit multiply).  VEC: 8-byte vectors of V = 8/itemsize samples (the
 // host checked that no vector straddles a row and all are aligned: JobArgs::vec8), thread t owns
 // vectors t + 256k; otherwise one element per lane, samples t + 256k.  Returns per-thread OR/min/max.
-template <int SRC, bool VEC>
+template <int SRC, bool VEC, typename SmpT>
 __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                               const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
+                                               const NormParams& np, const int32_t* lut, SmpT* smp, uint32_t& orv,
                                                int32_t& vmin, int32_t& vmax) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
@@ -192,7 +192,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       for (int k = 0; k < K; k++) {
         const int i = sidx_of(k);
         if (i < n) {
-          smp[sidx(i)] = v[k];
+          smp[sidx(i)] = (SmpT)v[k];
           orv |= (uint32_t)v[k];
           vmin = min(vmin, v[k]);
           vmax = max(vmax, v[k]);
@@ -208,37 +208,38 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       int32_t v;
       if (np.mode == 0) v = (int32_t)raw[k];
       else v = norm_sample<SRC>((double)raw[k], np);
-      smp[sidx(i)] = v;
+      smp[sidx(i)] = (SmpT)v;
       orv |= (uint32_t)v;
       vmin = min(vmin, v);
       vmax = max(vmax, v);
     }
   }
 }
+template <typename SmpT>
 __device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const StreamDev& st, const FrameDev& fr,
-                                             int c, const NormParams& np, const int32_t* lut, int32_t* smp,
+                                             int c, const NormParams& np, const int32_t* lut, SmpT* smp,
                                              uint32_t& orv, int32_t& vmin, int32_t& vmax) {
   if (vec8) {
     switch (src) {  // wave-uniform dispatch; f64 never takes the vector path
-      case ST_U8: load_channel_t<ST_U8, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I8: load_channel_t<ST_I8, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_U16: load_channel_t<ST_U16, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I16: load_channel_t<ST_I16, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_U32: load_channel_t<ST_U32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I32: load_channel_t<ST_I32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_F32: load_channel_t<ST_F32, true>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U8: load_channel_t<ST_U8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I8: load_channel_t<ST_I8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U16: load_channel_t<ST_U16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I16: load_channel_t<ST_I16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U32: load_channel_t<ST_U32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_I32: load_channel_t<ST_I32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_F32: load_channel_t<ST_F32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
       default: break;
     }
   }
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_channel_t<ST_U8, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I8: load_channel_t<ST_I8, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U16: load_channel_t<ST_U16, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I16: load_channel_t<ST_I16, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U32: load_channel_t<ST_U32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I32: load_channel_t<ST_I32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_F32: load_channel_t<ST_F32, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    default: load_channel_t<ST_F64, false>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U8: load_channel_t<ST_U8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I8: load_channel_t<ST_I8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U16: load_channel_t<ST_U16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I16: load_channel_t<ST_I16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U32: load_channel_t<ST_U32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_I32: load_channel_t<ST_I32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_F32: load_channel_t<ST_F32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    default: load_channel_t<ST_F64, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
   }
 }
 
@@ -675,16 +676,16 @@ __device__ __forceinline__ int64_t gres(const int32_t* x, int jj, const int32_t*
   }
 }
 // the same predictor read from the LDS sample array (slow path: irregular frames only)
-template <bool B32, int MAXO>
-__device__ __forceinline__ int64_t gres_lds(const int32_t* smp, int i, const int32_t* q, int sh) {
+template <bool B32, int MAXO, typename SmpT>
+__device__ __forceinline__ int64_t gres_lds(const SmpT* smp, int i, const int32_t* q, int sh) {
   if constexpr (B32) {
     int64_t sum = 0;
     for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[sidx(max(0, i - 1 - j))];
     return (int64_t)smp[sidx(i)] - (sum >> sh);
   } else {
     int32_t sum = 0;
-    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], smp[sidx(max(0, i - 1 - j))]);
-    return (int64_t)(smp[sidx(i)] - (sum >> sh));
+    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], (int32_t)smp[sidx(max(0, i - 1 - j))]);
+    return (int64_t)((int32_t)smp[sidx(i)] - (sum >> sh));
   }
 }
 
