@@ -186,6 +186,30 @@ __device__ __forceinline__ uint32_t lpc_abs16(const int32_t* x, const int32_t* q
   return acc;
 }
 
+// FRA-1 3.7: the two FIXED orders with the smallest block total of 2|r| (first minimum first; invalid
+// orders skipped) == oracle fg1/fg2.  Wave-uniform, every wave may run it.
+__device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kMaxPart], const int32_t* mvalid, int P,
+                                             int lane, int& g1, int& g2) {
+  uint64_t T[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    uint64_t v = lane < (1 << P) ? psum[k][lane] : 0ull;
+    v = up_add64<0>(v); v = up_add64<1>(v); v = up_add64<2>(v);
+    v = up_add64<3>(v); v = up_add64<4>(v); v = up_add64<5>(v);
+    T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  }
+  g1 = -1;
+  g2 = -1;
+  uint64_t b1 = 0, b2 = 0;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    if (!__builtin_amdgcn_readfirstlane(mvalid[k])) continue;
+    if (g1 < 0 || T[k] < b1) { b2 = b1; g2 = g1; b1 = T[k]; g1 = k; }
+    else if (g2 < 0 || T[k] < b2) { b2 = T[k]; g2 = k; }
+  }
+}
+
 // Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at
 // lane 2^p + j (level P = 6 nodes in a second register), so each lane runs ONE Rice estimate and
 // the per-level totals come out of a single upper-lane DPP chain (level p's segment is the aligned
@@ -441,8 +465,12 @@ read_x28(S.smp, t, x);
         }
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi & 1][wv], lane);
         __syncthreads();
-        if (early && wi == 0 && wv != 0) {  // FIXED 0..4 over waves 1-3 while wave 0 runs the LD below
-          for (int m = wv - 1; m < 5; m += 3) {
+        if (early && wi == 0 && (wv == 1 || wv == 2)) {  // the two FIXED candidates while wave 0 runs the LD
+          int g1, g2;
+          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
+          if (wv == 1 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
+          const int m = wv == 1 ? g1 : g2;
+          if (m >= 0) {
             const int pm = max_porder(n, m, cfg.max_porder);
             uint64_t best = 0;
             int bp = pm;
@@ -592,8 +620,13 @@ read_x28(S.smp, t, x);
 
   FRA_STOP(3)
   // ---- 5. every partition order of a model in one pass (one wave per model)
+  int fg1 = -1, fg2 = -1;
+  if (!early) {  // FIXED candidates (3.7): excluded orders are invalidated before the winner barrier
+    fixed_guess2(S.u.psum, S.mvalid, P, lane, fg1, fg2);
+    if (wv == 0 && lane < 5 && lane != fg1 && lane != fg2) S.mvalid[lane] = 0;
+  }
   for (int m = (early ? 5 : 0) + wv; m < nmod; m += 4) {
-    if (!S.mvalid[m]) continue;
+    if (!S.mvalid[m] || (m < 5 && m != fg1 && m != fg2)) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;

@@ -528,9 +528,23 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
   int bk[256];
   uint64_t best_est = 0;
 
-  /* candidate list: FIXED 0..4 then one LPC order per window */
+  /* candidate list: the two FIXED orders 0..4 with the smallest sum of 2|r| over the block (first
+   * minimum first, like libFLAC's fixed-order guess but keeping the runner-up), then one LPC order
+   * per window */
   int fmax = n - 1 < 4 ? n - 1 : 4;
+  int fg1 = -1, fg2 = -1;
+  {
+    uint64_t bt1 = 0, bt2 = 0;
+    for (int o = 0; o <= fmax; o++) {
+      if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue;
+      uint64_t T = 0;
+      for (int i = o; i < n; i++) T += 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
+      if (fg1 < 0 || T < bt1) { bt2 = bt1; fg2 = fg1; bt1 = T; fg1 = o; }
+      else if (fg2 < 0 || T < bt2) { bt2 = T; fg2 = o; }
+    }
+  }
   for (int o = 0; o <= fmax; o++) {
+    if (o != fg1 && o != fg2) continue;
     if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue; /* 32-bps: residual outside int32 */
     int po, kk[256];
     uint64_t e = hdr + (uint64_t)o * sbps + residual_estimate(r, n, o, cfg->max_porder, &po, kk);
