@@ -22,6 +22,7 @@ constexpr int kMaxBlock = 4096;   // samples per frame handled by one workgroup 
 constexpr int kThreads = 256;     // 4 waves; each thread owns 16 consecutive samples
 constexpr int kChunk = 16;        // samples per thread (also the FRA-1 autocorrelation chunk)
 constexpr int kMaxLpc = 12;
+constexpr int kMaxChannels = 8;  // FLAC channel limit (RFC 9639)
 constexpr int kMaxPart = 64;      // 2^6 partitions (level 6-8 max partition order)
 constexpr int kMaxWin = 6;        // subdivide_tukey(3): 1 + 2 + 3 windows
 constexpr int kMaxModels = 5 + kMaxWin;  // fixed 0..4, one LPC order per apodization window

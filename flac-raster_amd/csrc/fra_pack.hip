@@ -17,21 +17,25 @@
 // front pad (and the A bytes before F, which read as zero) are leading zeros, which leave a
 // zero-initialised CRC unchanged.  The 256 accumulators are combined by a DPP upper-lane tree
 // (x^(32*2^l) multipliers, host-precomputed byte tables), then the < 4 tail bytes byte-wise.
+#include <algorithm>
+
 #include "fra_device.h"
 
 namespace fra {
 
-// multiply a CRC-16 remainder by x^(8*2^i) mod P: two byte-table lookups
+// multiply a CRC-16 remainder by x^(8*2^i) mod P: two byte-table lookups (M = the LDS copy of levels
+// 2..10 of the host tables, i.e. M + (i - 2) * 512)
 __device__ __forceinline__ uint32_t crc_mul(const uint16_t* M, int i, uint32_t c) {
-  const uint16_t* m = M + (size_t)i * 512;
+  const uint16_t* m = M + (size_t)(i - 2) * 512;
   return (uint32_t)m[c & 0xFF] ^ (uint32_t)m[256 + (c >> 8)];
 }
 
 struct AssembleSmem {
   uint16_t T[4][256];   // slice-by-4: T[k][v] = CRC of v followed by k zero bytes
-  uint16_t MH[2][256];  // multiply by x^(32*256) (Horner step)
+  uint16_t M[9][512];   // multiply by x^(8*2^i), i = 2..10 (combine steps; i = 10 = x^(32*256): Horner)
+  uint8_t C8[256];      // CRC-8 (poly 0x07) byte table for the frame header
   uint32_t hdrw[8];     // frame header (+CRC-8) as big-endian words
-  uint32_t seg[8 + 2];  // seg[0] = 0, seg[1] = header bits, seg[c+2] = end of channel c
+  uint32_t seg[kMaxChannels + 2];  // seg[0] = 0, seg[1] = header bits, seg[c+2] = end of channel c
   uint32_t crcw[4];
 };
 
@@ -41,12 +45,20 @@ __device__ __forceinline__ uint32_t bits_at(const uint32_t* w, uint32_t b, int t
   return (uint32_t)((X << (b & 31)) >> (64 - take));
 }
 
+// one workgroup per frame; the CRC tables (slice-by-4, the combine multipliers, CRC-8) are copied to
+// LDS up front so no step of the CRC chain waits on a global gather
 __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
-  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (int i = t; i < 1024; i += kThreads) (&S.T[0][0])[i] = a.crctab[i];
-  const uint16_t* M = a.crctab + 1024;
-  for (int i = t; i < 512; i += kThreads) (&S.MH[0][0])[i] = M[10 * 512 + i];  // x^(8*2^10) = x^(32*256)
+  for (int i = t; i < 9 * 512; i += kThreads) (&S.M[0][0])[i] = a.crctab[1024 + 2 * 512 + i];
+  {
+    uint32_t c8 = (uint32_t)t;
+    for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) : (c8 << 1);
+    S.C8[t] = (uint8_t)c8;
+  }
+  const uint16_t* M = &S.M[0][0];
+  const int g = blockIdx.x;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   const int C = st.channels;
@@ -54,11 +66,7 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
     uint8_t h[24];
     int hl = frame_header(h, st, fr);
     uint32_t c8 = 0;
-    for (int i = 0; i < hl; i++) {
-      c8 ^= h[i];
-      for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) : (c8 << 1);
-      c8 &= 0xFF;
-    }
+    for (int i = 0; i < hl; i++) c8 = S.C8[(c8 ^ h[i]) & 0xFF];
     h[hl++] = (uint8_t)c8;
     for (int j = 0; j < 8; j++) S.hdrw[j] = 0;
     for (int b = 0; b < hl; b++) S.hdrw[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
@@ -99,23 +107,59 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
     return res;
   };
 
+  // Fast gather: a dword whose 32 bits lie inside ONE channel blob is a funnel shift of two adjacent
+  // slot words.  U dwords per thread are resolved and their loads issued together (latency overlap);
+  // dwords touching the header, a blob boundary or the frame ends take window() (a few per frame).
+  constexpr int U = 4;
+  uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
+#pragma unroll
+  for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = i <= C + 1 ? S.seg[i] : 0xFFFFFFFFu;
   uint32_t acc = 0;
-  int64_t k = (int64_t)t - pad;
-  if (k < 0) k += kThreads;
-  for (; k < ND; k += kThreads) {
-    const uint32_t val = window(8 * (4 * k - (int64_t)A));
-    if ((k > 0 || A == 0) && k < NF) {
-      gw[k] = __builtin_bswap32(val);
-    } else {
-      for (int b = 0; b < 4; b++) {
-        const int64_t fb = 4 * k - (int64_t)A + b;  // frame byte index
-        if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val >> (24 - 8 * b));
+  int64_t k0 = (int64_t)t - pad;
+  if (k0 < 0) k0 += kThreads;
+  for (; k0 < ND; k0 += (int64_t)kThreads * U) {
+    uint32_t w0[U], w1[U], sh[U];
+    bool fast[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t k = k0 + (int64_t)u * kThreads;
+      const int64_t bp = 8 * (4 * k - (int64_t)A);
+      fast[u] = false;
+      w0[u] = w1[u] = sh[u] = 0;
+      if (k < ND && bp >= (int64_t)sg[1] && bp + 32 <= (int64_t)TB) {
+        const uint32_t b = (uint32_t)bp;
+        int sgi = 1;  // blob sgi - 1 holds bit b: sg[sgi] <= b < sg[sgi + 1]
+#pragma unroll
+        for (int i = 2; i <= kMaxChannels + 1; i++) sgi += (b >= sg[i]) ? 1 : 0;
+        if (b + 32 <= sg[sgi + 1]) {
+          const uint32_t rel = b - sg[sgi];
+          const uint32_t* src = slots + (size_t)(sgi - 1) * a.tmp_stride + (rel >> 5);
+          w0[u] = src[0];
+          w1[u] = src[1];
+          sh[u] = rel & 31;
+          fast[u] = true;
+        }
       }
     }
-    if (k < NF) {
-      const uint32_t c4 = (uint32_t)S.T[3][val >> 24] ^ (uint32_t)S.T[2][(val >> 16) & 0xFF] ^
-                          (uint32_t)S.T[1][(val >> 8) & 0xFF] ^ (uint32_t)S.T[0][val & 0xFF];
-      acc = ((uint32_t)S.MH[0][acc & 0xFF] ^ (uint32_t)S.MH[1][acc >> 8]) ^ c4;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t k = k0 + (int64_t)u * kThreads;
+      if (k >= ND) break;
+      const uint32_t val = fast[u] ? (uint32_t)((((uint64_t)w0[u] << 32) | w1[u]) >> (32 - sh[u]))
+                                   : window(8 * (4 * k - (int64_t)A));
+      if ((k > 0 || A == 0) && k < NF) {
+        gw[k] = __builtin_bswap32(val);
+      } else {
+        for (int b = 0; b < 4; b++) {
+          const int64_t fb = 4 * k - (int64_t)A + b;  // frame byte index
+          if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val >> (24 - 8 * b));
+        }
+      }
+      if (k < NF) {
+        const uint32_t c4 = (uint32_t)S.T[3][val >> 24] ^ (uint32_t)S.T[2][(val >> 16) & 0xFF] ^
+                            (uint32_t)S.T[1][(val >> 8) & 0xFF] ^ (uint32_t)S.T[0][val & 0xFF];
+        acc = crc_mul(M, 10, acc) ^ c4;  // Horner step: x^(32*256)
+      }
     }
   }
   // combine: lane order == virtual dword order; left groups are multiplied by x^(32*2^l)
