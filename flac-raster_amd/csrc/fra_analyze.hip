@@ -81,7 +81,14 @@ __device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)
   }
 }
 
-template <bool B32>
+// windows per block at this lag bound (levels 3-6: <= 3 with max_lpc 8; levels 7-8: <= 6) and the
+// waves that run Levinson-Durbin (window wi on wave wi % 4)
+template <int MAXLAG>
+constexpr int kWinCap() { return MAXLAG == 0 ? 1 : (MAXLAG <= 8 ? 3 : kMaxWin); }
+template <int MAXLAG>
+constexpr int kLdWaves() { return kWinCap<MAXLAG>() < 4 ? kWinCap<MAXLAG>() : 4; }
+
+template <bool B32, int MAXLAG>
 struct AnalyzeSmem {
   // sample i at sidx(i); [0, kSmpStride) = zero chunk.  16-bit path: int16 (every sample fits), which
   // keeps the workgroup at <= 32 KiB LDS (5 workgroups per CU at 96 VGPRs)
@@ -92,9 +99,9 @@ struct AnalyzeSmem {
   } u;
   unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
   unsigned long long esum2[kMaxPart][3];     // fast frames: exact-pass sums of u >> (k0-1), u >> k0, u >> (k0+1)
-  double red[2][4][kMaxLpc + 1];  // double-buffered by window parity
+  double red[kWinCap<MAXLAG>()][4][MAXLAG + 1];  // per window, per wave: reduced chunk partials
   double autoc[kMaxLpc + 1];
-  double lp[kMaxLpc][kMaxLpc];
+  double lp[kLdWaves<MAXLAG>()][MAXLAG > 0 ? MAXLAG : 1][MAXLAG > 0 ? MAXLAG : 1];  // LD rows per LD wave
   double err[kMaxLpc];
   int32_t mcoef[kMaxModels][kMaxLpc];
   int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
@@ -147,6 +154,29 @@ __device__ __forceinline__ uint64_t lpc_sum_fast(const int32_t* x, const int32_t
 #pragma unroll
   for (int jj = 0; jj < kChunk; jj++) acc_zz<B32>(gres<B32, O>(x, jj, q, sh), jj >= skip, acc, ovf);
   return acc;
+}
+
+// 32-bps path: the predictor evaluated exactly in double precision: |q| < 2^14 (precision <= 15) and
+// |x| < 2^31, so every product and partial sum is an integer below 2^50 (exact in f64);
+// floor(sum * 2^-sh) is the int64 arithmetic shift and x - pred is exact.  Sum of 2|r| over the
+// thread's samples (warm-up positions jj < skip masked); ovf if a residual leaves int32 (model invalid,
+// as the oracle's compute_residual).  Replaces ~3 integer instructions per 64-bit multiply-add.
+template <int O>
+__device__ __forceinline__ uint64_t lpc_abs2_f64(const double* xd, const double* qd, int sh, int skip, bool& ovf) {
+  const double scale = ldexp(1.0, -sh);
+  double acc = 0.0;  // exact: sum of 16 |r| < 2^35 whenever no residual overflowed
+#pragma unroll
+  for (int jj = 0; jj < kChunk; jj++) {
+    const int b = 12 + jj;
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < O; j++) sum = fma(qd[j], xd[b - 1 - j], sum);
+    const double r = xd[b] - floor(sum * scale);
+    const bool on = jj >= skip;
+    ovf |= on && (r > 2147483647.0 || r < -2147483648.0);
+    acc += on ? fabs(r) : 0.0;
+  }
+  return ovf ? 0ull : 2ull * (uint64_t)acc;
 }
 
 // 16-bit path LPC predictor with v_dot2c_i32_i16: samples fit int16 and |q| < 2^11, so the pairwise
@@ -288,7 +318,7 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : 5) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
-  __shared__ AnalyzeSmem<B32> S;
+  __shared__ AnalyzeSmem<B32, MAXLAG> S;
   const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
@@ -316,14 +346,6 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : 5) k_analyze(JobArgs a, in
     const NormParams np = norm_params(st, a.norm[fr.stream]);
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
     load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
-  }
-  // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window:
-  // issued here so their latency hides under the reductions and the barrier below
-  float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
-  if constexpr (MAXLAG > 0) {
-    const float* win = a.win + (size_t)fr.win * a.nwin * a.blocksize;
-#pragma unroll
-    for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[t * kChunk + j];  // table padded by kMaxLpc
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -421,10 +443,20 @@ read_x28(S.smp, t, x);
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = !B32 && fastframe && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
 
+  // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window
+  float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
+  if constexpr (MAXLAG > 0) {
+    const float* win = a.win + (size_t)fr.win * a.nwin * a.blocksize;
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[t * kChunk + j];  // table padded by kMaxLpc
+  }
   // ---- 3. LPC analysis per apodization window (3.4-3.7)
   const int prec = qlp_precision(bps, n);
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
+      if constexpr (MAXLAG <= 8) {
+        // levels 3-6 (<= 3 windows): window by window, wave 0 runs Levinson-Durbin while waves 1-3
+        // run ahead (lowest register pressure: the 5-waves/SIMD configuration has no spills)
       // one apodization window: windowed samples -> chunk partials -> wave reduce-scatter -> barrier ->
       // (window 0: FIXED searches on waves 1-3) + wave 0's Levinson-Durbin / order / quantisation.
       // Window 0 is peeled so its prefetched coefficients are dead after its first use (no live range
@@ -494,7 +526,7 @@ read_x28(S.smp, t, x);
           const int m = 5 + wi;
           int nord = 0;
           double errv[MAXLAG];
-          if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp, errv, lane == 0);
+          if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[0], errv, lane == 0);
           bool ok = false;
           int o = 0, sh = 0;
           int32_t q[MAXLAG];
@@ -514,7 +546,7 @@ read_x28(S.smp, t, x);
             __builtin_amdgcn_wave_barrier();
             double lpo[MAXLAG];
 #pragma unroll
-            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[o - 1][j];
+            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[0][o - 1][j];
             ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
           }
           if (lane == 0) {
@@ -533,6 +565,120 @@ read_x28(S.smp, t, x);
         for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
         window_pass(wi, wl);
       }
+          } else {
+        // levels 7-8 (up to 6 windows): every window's autocorrelation first, then Levinson-Durbin of
+        // window wi on wave wi % 4 in parallel
+      // 3.1 autocorrelation of every window: windowed samples -> chunk partials -> wave
+      // reduce-scatter -> red[wi][wave][lag].  Window 0 is peeled so its prefetched coefficients die
+      // at their first use.
+      auto window_acf = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG]) {
+        float wf[kChunk + MAXLAG];
+        {
+          int32_t y[kChunk + 8];
+          read_y24(S.smp, t, y);
+#pragma unroll
+          for (int j = 0; j < kChunk + MAXLAG; j++) {
+            const int i = i0 + j;
+            const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
+            wf[j] = (i < n) ? (float)v * wcoef[j] : 0.0f;
+          }
+        }
+
+        // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
+        // float*float product, so this is bit-identical to the oracle's acc + a*b
+        double acc[MAXLAG + 1];
+#pragma unroll
+        for (int l = 0; l <= MAXLAG; l++) acc[l] = 0.0;
+        if (i0 + kChunk + MAXLAG <= n) {
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) {
+            const double a0 = (double)wf[jj];
+#pragma unroll
+            for (int l = 0; l <= MAXLAG; l++) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
+          }
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) {
+            const double a0 = (double)wf[jj];
+#pragma unroll
+            for (int l = 0; l <= MAXLAG; l++)
+              if (i0 + jj + l < n) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
+          }
+        }
+        autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi][wv], lane);
+      };
+      window_acf(0, wcur);
+      for (int wi = 1; wi < a.nwin; wi++) {
+        float wl[kChunk + MAXLAG];
+        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+#pragma unroll
+        for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
+        window_acf(wi, wl);
+      }
+      __syncthreads();
+      // 3.2 (fast 16-bit frames) the two FIXED candidates, searched on the two waves after the ones
+      // running Levinson-Durbin (psum is complete since the barrier above)
+      if (early) {
+        const int j = (wv - a.nwin % 4 + 4) % 4;  // this wave's slot after the LD waves
+        if (j < 2) {
+          int g1, g2;
+          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
+          if (j == 0 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
+          const int m = j == 0 ? g1 : g2;
+          if (m >= 0) {
+            const int pm = max_porder(n, m, cfg.max_porder);
+            uint64_t best = 0;
+            int bp = pm;
+            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
+            if (lane == 0) {
+              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
+              S.mporder[m] = bp;
+            }
+          }
+        }
+      }
+      // 3.3 window wi on wave wi % 4, uniformly: autocorrelation -> Levinson-Durbin (registers) ->
+      // expected bits of every order in parallel (lane o) -> first minimum -> qlp quantisation
+      for (int wi = wv; wi < a.nwin; wi += 4) {
+        double ac[MAXLAG + 1];
+#pragma unroll
+        for (int l = 0; l <= MAXLAG; l++)
+          ac[l] = l <= lmax ? (S.red[wi][0][l] + S.red[wi][1][l]) + (S.red[wi][2][l] + S.red[wi][3][l])
+                                : 0.0;
+        const int m = 5 + wi;
+        int nord = 0;
+        double errv[MAXLAG];
+        if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[wv], errv, lane == 0);
+        bool ok = false;
+        int o = 0, sh = 0;
+        int32_t q[MAXLAG];
+        if (nord > 0) {
+          double e = errv[0];
+#pragma unroll
+          for (int j = 1; j < MAXLAG; j++)
+            if (lane == j + 1) e = errv[j];
+          // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as
+          // an unsigned integer; DPP min over the wave, lowest lane among the equal ones
+          const bool on = lane >= 1 && lane <= nord;
+          const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lane, prec + sbps)) : ~0ull;
+          const uint64_t kmin = wave_min64(key);
+          o = (int)__builtin_ctzll(__ballot(on && key == kmin));
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's lp rows -> all lanes
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_wave_barrier();
+          double lpo[MAXLAG];
+#pragma unroll
+          for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[wv][o - 1][j];
+          ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
+        }
+        if (lane == 0) {
+          S.mvalid[m] = ok ? 1 : 0;
+          S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
+#pragma unroll
+          for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
+        }
+          }
+      }
     }
   }
 
@@ -542,17 +688,18 @@ read_x28(S.smp, t, x);
 read_x28(S.smp, t, x);
   }
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
+  double xd[B32 ? 12 + kChunk : 1];  // 32-bps fast path: x as exact doubles
   if (fastframe) {
     if constexpr (B32) {
-      // 32-bps: FIXED k as the 4-tap integer predictor (int64), one model at a time
-      for (int m = 0; m < 5; m++) {
-        const int o = m;
-        int32_t q[4];
+      // 32-bps: FIXED k as the 4-tap predictor [1] [2,-1] [3,-3,1] [4,-6,4,-1], exact in f64
 #pragma unroll
-        for (int j = 0; j < 4; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
-        const int skip = o > i0 ? o - i0 : 0;
+      for (int j = 0; j < 12 + kChunk; j++) xd[j] = (double)x[j];
+#pragma unroll
+      for (int m = 0; m < 5; m++) {
+        constexpr double kF[5][4] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, -1, 0, 0}, {3, -3, 1, 0}, {4, -6, 4, -1}};
+        const int skip = m > i0 ? m - i0 : 0;
         bool ovf = false;
-        const uint64_t acc = lpc_sum_fast<true, 4>(x, q, 0, skip, ovf);
+        const uint64_t acc = lpc_abs2_f64<4>(xd, kF[m], 0, skip, ovf);
         if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;
       }
@@ -565,6 +712,9 @@ read_x28(S.smp, t, x);
       int32_t q[MAXO];
 #pragma unroll
       for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+      double qd[MAXO];  // (32-bps path)
+#pragma unroll
+      for (int j = 0; j < MAXO; j++) qd[j] = (double)q[j];
       const int skip = o > i0 ? o - i0 : 0;
       bool ovf = false;
       uint64_t acc = 0;
@@ -572,7 +722,7 @@ read_x28(S.smp, t, x);
 #define FRA_CASE(O_) \
   case O_:           \
     if constexpr (O_ <= MAXO) { \
-      if constexpr (B32) acc = lpc_sum_fast<B32, O_>(x, q, sh, skip, ovf); \
+      if constexpr (B32) acc = lpc_abs2_f64<O_>(xd, qd, sh, skip, ovf); \
       else acc = 2ull * lpc_abs16<O_>(x, q, sh, head); \
     } \
     break;

@@ -475,7 +475,7 @@ __device__ inline int best_order_by_error(const double* err, int norders, int n,
 // stay in registers (errv), coefficient rows go to LDS from lane 0 only.  Same op sequence as
 // oracle ora_levinson.
 template <int MAXLAG>
-__device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_order, double (*lp)[kMaxLpc],
+__device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_order, double (*lp)[MAXLAG],
                                     double (&errv)[MAXLAG], bool writer) {
   double lpc[MAXLAG];
 #pragma unroll
