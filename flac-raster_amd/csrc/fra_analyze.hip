@@ -589,7 +589,13 @@ read_x28(S.smp, t, x);
         double acc[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++) acc[l] = 0.0;
-        if (i0 + kChunk + MAXLAG <= n) {
+        // partial windows are zero outside their segment: a wave whose windowed samples are all zero
+        // keeps every partial at +0.0 (exact products of zeros sum to +0), so it skips the FMAs
+        bool nz = false;
+#pragma unroll
+        for (int j = 0; j < kChunk + MAXLAG; j++) nz |= wf[j] != 0.0f;
+        if (!__any(nz)) {
+        } else if (i0 + kChunk + MAXLAG <= n) {
 #pragma unroll
           for (int jj = 0; jj < kChunk; jj++) {
             const double a0 = (double)wf[jj];
