@@ -92,6 +92,7 @@ struct fra_plan {
   size_t scan_tmp_bytes = 0;
   uint16_t* d_crctab = nullptr;
   uint32_t* d_tmp = nullptr;
+  uint32_t* d_fmeta = nullptr;
   int32_t* d_lut = nullptr;
   int64_t tmp_stride = 0;
   JobArgs args{};
@@ -241,6 +242,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_scan_tmp);
   (void)hipFree(p->d_crctab);
   (void)hipFree(p->d_tmp);
+  (void)hipFree(p->d_fmeta);
   (void)hipFree(p->d_lut);
   for (auto& e : p->ev)
     if (e) (void)hipEventDestroy(e);
@@ -372,6 +374,7 @@ static int plan_build(fra_plan* p) {
   // per-subframe slots for the encoded subframes (k_analyze -> k_assemble)
   p->tmp_stride = ((int64_t)j.blocksize * bps + 64 + 31) / 32 + 4;
   HIPCHK(hipMalloc(&p->d_tmp, sizeof(uint32_t) * (size_t)p->tmp_stride * std::max(1, nfr) * p->cmax));
+  HIPCHK(hipMalloc(&p->d_fmeta, sizeof(uint32_t) * kMetaWords * std::max(1, nfr)));
   {
     const std::vector<uint16_t> ct = crc16_tables();
     HIPCHK(hipMalloc(&p->d_crctab, sizeof(uint16_t) * ct.size()));
@@ -395,6 +398,7 @@ static int plan_build(fra_plan* p) {
   a.out = p->d_out;
   a.crctab = p->d_crctab;
   a.tmp = p->d_tmp;
+  a.fmeta = p->d_fmeta;
   a.tmp_stride = p->tmp_stride;
   a.lut = p->d_lut;
   a.lut_stride = lut_stride;

@@ -166,6 +166,13 @@ struct SfDesc {
   uint8_t k[kMaxPart];
 };
 
+// per-frame metadata written by k_frame_bytes for k_assemble: words [0, kHdrWords) = frame header and
+// its CRC-8 as big-endian words (zero padded), words [kHdrWords, +kMaxChannels+2) = bit bounds:
+// 0, header bits, end of channel 0, ..., end of channel C-1 (unused entries = 0xFFFFFFFF)
+constexpr int kHdrWords = 6;
+constexpr int kMetaWords = 16;
+static_assert(kHdrWords + kMaxChannels + 2 <= kMetaWords, "frame metadata layout");
+
 struct JobArgs {
   const void* raster;
   const StreamDev* streams;
@@ -177,6 +184,7 @@ struct JobArgs {
   unsigned long long* frame_off;  // [nframes_total + 1] exclusive scan of frame_bytes
   uint8_t* out;            // concatenated frames
   const uint16_t* crctab;  // CRC-16 slice-by-4 tables [4][256] + multiply-by-x^(8*2^i) tables [24][2][256]
+  uint32_t* fmeta;         // [nframes_total][kMetaWords]: header (+CRC-8) as big-endian words, blob bit bounds
   uint32_t* tmp;           // encoded subframes: slot (frame*cmax + channel) of tmp_stride words
   const int32_t* lut;      // normalize_to_audio table per stream (<= 16-bit integer dtypes), or null
   int64_t lut_stride;      // entries per stream: 256 (8-bit) or 65536 (16-bit); entry d = sample of mn + d

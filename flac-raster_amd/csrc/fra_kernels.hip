@@ -167,9 +167,28 @@ __global__ void k_frame_bytes(JobArgs a) {
   if (g == a.nframes_total) { a.frame_bytes[g] = 0; return; }  // scan input tail
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
-  uint64_t bits = (uint64_t)frame_header_len(st, fr) * 8;
-  for (int c = 0; c < st.channels; c++) bits += a.sf[(size_t)g * a.cmax + c].bits;
-  a.frame_bytes[g] = ((bits + 7) >> 3) + 2;
+  uint8_t h[4 * kHdrWords];
+  int hl = frame_header(h, st, fr);
+  uint32_t c8 = 0;  // CRC-8, poly x^8+x^2+x+1, init 0 (RFC 9639 9.1.8)
+  for (int i = 0; i < hl; i++) {
+    c8 ^= h[i];
+    for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) & 0xFF : (c8 << 1);
+  }
+  h[hl++] = (uint8_t)c8;
+  uint32_t* m = a.fmeta + (size_t)g * kMetaWords;
+  uint32_t w[kHdrWords] = {};
+  for (int b = 0; b < hl; b++) w[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
+#pragma unroll
+  for (int j = 0; j < kHdrWords; j++) m[j] = w[j];
+  uint32_t bits = (uint32_t)hl * 8;
+  m[kHdrWords] = 0;
+  m[kHdrWords + 1] = bits;
+#pragma unroll
+  for (int c = 0; c < kMaxChannels; c++) {
+    if (c < st.channels) bits += a.sf[(size_t)g * a.cmax + c].bits;
+    m[kHdrWords + 2 + c] = c < st.channels ? bits : 0xFFFFFFFFu;
+  }
+  a.frame_bytes[g] = ((uint64_t)(bits + 7) >> 3) + 2;
 }
 
 // ============================================================================ launchers

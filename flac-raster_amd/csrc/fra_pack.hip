@@ -30,13 +30,12 @@ __device__ __forceinline__ uint32_t crc_mul(const uint16_t* M, int i, uint32_t c
   return (uint32_t)m[c & 0xFF] ^ (uint32_t)m[256 + (c >> 8)];
 }
 
-struct AssembleSmem {
+struct alignas(16) AssembleSmem {
   uint16_t T[4][256];   // slice-by-4: T[k][v] = CRC of v followed by k zero bytes
   uint16_t M[9][512];   // multiply by x^(8*2^i), i = 2..10 (combine steps; i = 10 = x^(32*256): Horner)
-  uint8_t C8[256];      // CRC-8 (poly 0x07) byte table for the frame header
-  uint32_t hdrw[8];     // frame header (+CRC-8) as big-endian words
-  uint32_t seg[kMaxChannels + 2];  // seg[0] = 0, seg[1] = header bits, seg[c+2] = end of channel c
+  uint32_t meta[kMetaWords];  // this frame's header words and blob bit bounds (k_frame_bytes)
   uint32_t crcw[4];
+  uint32_t tailw;       // the output window of the last, partial dword (bytes [4*NF - A, L))
 };
 
 // `take` (1..32) bits at bit b of a big-endian word array, right-aligned
@@ -45,39 +44,38 @@ __device__ __forceinline__ uint32_t bits_at(const uint32_t* w, uint32_t b, int t
   return (uint32_t)((X << (b & 31)) >> (64 - take));
 }
 
-// one workgroup per frame; the CRC tables (slice-by-4, the combine multipliers, CRC-8) are copied to
-// LDS up front so no step of the CRC chain waits on a global gather
-__global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
+// one workgroup per frame; the CRC tables (slice-by-4, the combine multipliers) are copied to LDS up
+// front (16-byte loads) so no step of the CRC chain waits on a global gather.  Header and blob bounds
+// come precomputed from k_frame_bytes, so every metadata load is issued in the first round.
+__global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int i = t; i < 1024; i += kThreads) (&S.T[0][0])[i] = a.crctab[i];
-  for (int i = t; i < 9 * 512; i += kThreads) (&S.M[0][0])[i] = a.crctab[1024 + 2 * 512 + i];
+  const int g = blockIdx.x;
   {
-    uint32_t c8 = (uint32_t)t;
-    for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) : (c8 << 1);
-    S.C8[t] = (uint8_t)c8;
+    const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab);
+    const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + 2 * 512);
+    uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
+    uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
+    constexpr int NT = 1024 * 2 / 16, NM = 9 * 512 * 2 / 16;
+    for (int i = t; i < NT + NM; i += kThreads) {
+      if (i < NT) dT[i] = srcT[i];
+      else dM[i - NT] = srcM[i - NT];
+    }
+    if (t < kMetaWords) S.meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
   }
   const uint16_t* M = &S.M[0][0];
-  const int g = blockIdx.x;
-  const FrameDev fr = a.frames[g];
-  const StreamDev st = a.streams[fr.stream];
-  const int C = st.channels;
-  if (t == 0) {
-    uint8_t h[24];
-    int hl = frame_header(h, st, fr);
-    uint32_t c8 = 0;
-    for (int i = 0; i < hl; i++) c8 = S.C8[(c8 ^ h[i]) & 0xFF];
-    h[hl++] = (uint8_t)c8;
-    for (int j = 0; j < 8; j++) S.hdrw[j] = 0;
-    for (int b = 0; b < hl; b++) S.hdrw[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
-    S.seg[0] = 0;
-    S.seg[1] = (uint32_t)hl * 8;
-    for (int c = 0; c < C; c++) S.seg[c + 2] = S.seg[c + 1] + a.sf[(size_t)g * a.cmax + c].bits;
-  }
+  const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform: scalar loads
+  auto rfl64 = [](uint64_t v) -> uint64_t {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+  };
+  const uint64_t F = rfl64(a.frame_off[g]);
+  const uint64_t L = rfl64(a.frame_bytes[g]) - 2;  // = ceil(TB / 8): bytes covered by the CRC-16
+  const int C = __builtin_amdgcn_readfirstlane(a.streams[a.frames[g].stream].channels);
   __syncthreads();
-  const uint32_t TB = S.seg[C + 1];             // frame bits before the byte pad
-  const uint64_t F = a.frame_off[g];
-  const uint64_t L = a.frame_bytes[g] - 2;      // = ceil(TB / 8): bytes covered by the CRC-16
+  const uint32_t* hdrw = S.meta;
+  const uint32_t* seg = S.meta + kHdrWords;
+  const uint32_t TB = seg[C + 1];               // frame bits before the byte pad
   const uint32_t A = (uint32_t)(F & 3);
   uint32_t* gw = (uint32_t*)(a.out + (F - A));  // dword k of this frame's span
   const int64_t ND = (int64_t)((F + L - 1) >> 2) - (int64_t)(F >> 2) + 1;  // dwords touching the frame
@@ -95,11 +93,11 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
     }
     int s = 0;
     while (filled < 32 && bp < (int64_t)TB) {
-      while ((int64_t)S.seg[s + 1] <= bp) s++;
-      const uint32_t take = (uint32_t)min<int64_t>(32 - filled, (int64_t)S.seg[s + 1] - bp);
-      const uint32_t rel = (uint32_t)(bp - S.seg[s]);
+      while ((int64_t)seg[s + 1] <= bp) s++;
+      const uint32_t take = (uint32_t)min<int64_t>(32 - filled, (int64_t)seg[s + 1] - bp);
+      const uint32_t rel = (uint32_t)(bp - seg[s]);
       const uint32_t v =
-          s == 0 ? bits_at(S.hdrw, rel, (int)take) : bits_at(slots + (size_t)(s - 1) * a.tmp_stride, rel, (int)take);
+          s == 0 ? bits_at(hdrw, rel, (int)take) : bits_at(slots + (size_t)(s - 1) * a.tmp_stride, rel, (int)take);
       res |= take == 32 ? v : (v << (32 - filled - (int)take));
       filled += (int)take;
       bp += take;
@@ -113,7 +111,7 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
   constexpr int U = 4;
   uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
 #pragma unroll
-  for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = i <= C + 1 ? S.seg[i] : 0xFFFFFFFFu;
+  for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = __builtin_amdgcn_readfirstlane(gmeta[kHdrWords + i]);
   uint32_t acc = 0;
   int64_t k0 = (int64_t)t - pad;
   if (k0 < 0) k0 += kThreads;
@@ -155,6 +153,7 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
           if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val >> (24 - 8 * b));
         }
       }
+      if (k == NF) S.tailw = val;
       if (k < NF) {
         const uint32_t c4 = (uint32_t)S.T[3][val >> 24] ^ (uint32_t)S.T[2][(val >> 16) & 0xFF] ^
                             (uint32_t)S.T[1][(val >> 8) & 0xFF] ^ (uint32_t)S.T[0][val & 0xFF];
@@ -178,7 +177,7 @@ __global__ void __launch_bounds__(kThreads) k_assemble(JobArgs a) {
     // tail: frame bytes [4*NF - A, L) not covered by whole dwords
     const int64_t tb0 = 4 * NF - (int64_t)A;
     if (tb0 < (int64_t)L) {
-      const uint32_t val = window(8 * tb0);
+      const uint32_t val = S.tailw;
       for (int64_t fb = tb0; fb < (int64_t)L; fb++) {
         const uint32_t by = (val >> (24 - 8 * (int)(fb - tb0))) & 0xFF;
         crc = ((crc << 8) ^ S.T[0][((crc >> 8) ^ by) & 0xFF]) & 0xFFFF;
