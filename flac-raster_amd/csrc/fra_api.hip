@@ -158,7 +158,7 @@ static uint32_t gf16_mul(uint32_t a, uint32_t b) {
   return r & 0xFFFFu;
 }
 static std::vector<uint16_t> crc16_tables() {
-  std::vector<uint16_t> tab(1024 + 24 * 512);
+  std::vector<uint16_t> tab(kCrcT16Off + 16 * 256);
   for (int v = 0; v < 256; v++) {
     uint32_t d = (uint32_t)v << 8;
     for (int b = 0; b < 8; b++) d = (d & 0x8000u) ? ((d << 1) ^ 0x8005u) : (d << 1);
@@ -168,6 +168,12 @@ static std::vector<uint16_t> crc16_tables() {
     for (int v = 0; v < 256; v++) {
       const uint32_t p = tab[(k - 1) * 256 + v];
       tab[k * 256 + v] = (uint16_t)(((p << 8) & 0xFFFFu) ^ tab[p >> 8]);
+    }
+  for (int k = 0; k < 16; k++)  // slice-by-16 (k_assemble): T16[k] = T[k] for k < 4
+    for (int v = 0; v < 256; v++) {
+      if (k == 0) { tab[kCrcT16Off + v] = tab[v]; continue; }
+      const uint32_t p = tab[kCrcT16Off + (k - 1) * 256 + v];
+      tab[kCrcT16Off + k * 256 + v] = (uint16_t)(((p << 8) & 0xFFFFu) ^ tab[p >> 8]);
     }
   uint32_t X = 0x100;  // x^8
   for (int i = 0; i < 24; i++) {

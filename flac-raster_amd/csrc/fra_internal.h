@@ -169,6 +169,9 @@ struct SfDesc {
 // per-frame metadata written by k_frame_bytes for k_assemble: words [0, kHdrWords) = frame header and
 // its CRC-8 as big-endian words (zero padded), words [kHdrWords, +kMaxChannels+2) = bit bounds:
 // 0, header bits, end of channel 0, ..., end of channel C-1 (unused entries = 0xFFFFFFFF)
+// CRC-16 table layout (fra_api.hip crc16_tables): [0, 1024) slice-by-4 byte tables, [1024, +24*512)
+// multiply-by-x^(8*2^i) tables, [kCrcT16Off, +16*256) slice-by-16 byte tables
+constexpr int kCrcT16Off = 1024 + 24 * 512;
 constexpr int kHdrWords = 6;
 constexpr int kMetaWords = 16;
 static_assert(kHdrWords + kMaxChannels + 2 <= kMetaWords, "frame metadata layout");

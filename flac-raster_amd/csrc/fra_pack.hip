@@ -6,33 +6,49 @@
 // frame header (RFC 9639 9.1, CRC-8) ++ subframes (9.2, encoded by k_analyze into per-subframe
 // slots) ++ zero pad to a byte ++ CRC-16.
 //
-// Gather formulation: every thread builds whole output dwords.  Global dword G0+k (G0 = F>>2)
-// holds frame bits [8(4k-A), +32) (A = F & 3): the header and the channel blobs are laid end to end
-// at known bit offsets, so each 32-bit window is a funnel-shifted read from at most a few segments.
-// Dwords entirely inside the frame are written with one aligned store; the first/last dwords
-// (shared with the neighbouring frames) get byte stores.
+// Gather formulation: every thread builds whole output quads (4 dwords, 16-byte aligned in the
+// output).  Global dword G0+k (G0 = (F-A)/4, A = F & 3) holds frame bits [8(4k-A), +32): the header
+// and the channel blobs are laid end to end at known bit offsets (k_frame_bytes), so a quad that lies
+// inside one blob is a funnel shift (one shift for all four) of 5 consecutive slot words: one 16-byte
+// load + one dword load + one 16-byte store.  Quads touching the header, a blob boundary or the frame
+// ends resolve dword by dword; the first/last dwords (shared with the neighbouring frames) get byte
+// stores.
 //
-// CRC-16 (poly x^16+x^15+x^2+1, init 0) on the same dwords, no extra pass: thread t folds the dwords
-// with virtual index v = k + pad == t (mod 256) by Horner (acc = acc * x^(32*256) ^ crc4(dword)); the
-// front pad (and the A bytes before F, which read as zero) are leading zeros, which leave a
-// zero-initialised CRC unchanged.  The 256 accumulators are combined by a DPP upper-lane tree
-// (x^(32*2^l) multipliers, host-precomputed byte tables), then the < 4 tail bytes byte-wise.
+// CRC-16 (poly x^16+x^15+x^2+1, init 0) on the same dwords, no extra pass.  Virtual dword v = k + a4
+// (a4 = G0 mod 4, so quads in v are the aligned output quads); virtual quad u = v/4 + pad, pad making
+// the last quad that holds CRC bytes land on thread 255.  Thread t folds the quads u == t (mod 256) by
+// Horner (acc = acc * x^(128*256) ^ crc16(quad), slice-by-16 tables): leading zeros (the pad and the A
+// bytes before F read as zero) leave a zero-initialised CRC unchanged; the e < 4 zero dwords after the
+// last whole CRC dword are removed by multiplying with x^(-32e).  The 256 accumulators are combined by
+// a DPP upper-lane tree (x^(128*2^l)), then the < 4 tail bytes byte-wise.
 #include <algorithm>
 
 #include "fra_device.h"
 
 namespace fra {
 
-// multiply a CRC-16 remainder by x^(8*2^i) mod P: two byte-table lookups (M = the LDS copy of levels
-// 2..10 of the host tables, i.e. M + (i - 2) * 512)
+constexpr int kMLo = 4, kMLevels = 9;  // LDS copy of multiply tables x^(8*2^i), i = 4..12
+
+// multiply a CRC-16 remainder by x^(8*2^i) mod P: two byte-table lookups
 __device__ __forceinline__ uint32_t crc_mul(const uint16_t* M, int i, uint32_t c) {
-  const uint16_t* m = M + (size_t)(i - 2) * 512;
+  const uint16_t* m = M + (size_t)(i - kMLo) * 512;
   return (uint32_t)m[c & 0xFF] ^ (uint32_t)m[256 + (c >> 8)];
 }
 
+// a * b mod P (bit-serial; one call per frame)
+__device__ __forceinline__ uint32_t gf16_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 15; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x10000u) r ^= 0x18005u;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r & 0xFFFFu;
+}
+
 struct alignas(16) AssembleSmem {
-  uint16_t T[4][256];   // slice-by-4: T[k][v] = CRC of v followed by k zero bytes
-  uint16_t M[9][512];   // multiply by x^(8*2^i), i = 2..10 (combine steps; i = 10 = x^(32*256): Horner)
+  uint16_t T[16][256];  // slice-by-16: T[k][v] = CRC of v followed by k zero bytes
+  uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..12 (tree 4..9, waves 10..11, Horner 12)
   uint32_t meta[kMetaWords];  // this frame's header words and blob bit bounds (k_frame_bytes)
   uint32_t crcw[4];
   uint32_t tailw;       // the output window of the last, partial dword (bytes [4*NF - A, L))
@@ -44,19 +60,23 @@ __device__ __forceinline__ uint32_t bits_at(const uint32_t* w, uint32_t b, int t
   return (uint32_t)((X << (b & 31)) >> (64 - take));
 }
 
-// one workgroup per frame; the CRC tables (slice-by-4, the combine multipliers) are copied to LDS up
-// front (16-byte loads) so no step of the CRC chain waits on a global gather.  Header and blob bounds
-// come precomputed from k_frame_bytes, so every metadata load is issued in the first round.
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32 - sh));
+}
+
+// one workgroup per frame; the CRC tables are copied to LDS up front (16-byte loads) so no step of
+// the CRC chain waits on a global gather.  Header and blob bounds come precomputed from
+// k_frame_bytes, so every metadata load is issued in the first round.
 __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = blockIdx.x;
   {
-    const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab);
-    const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + 2 * 512);
+    const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
+    const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
     uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
     uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
-    constexpr int NT = 1024 * 2 / 16, NM = 9 * 512 * 2 / 16;
+    constexpr int NT = 16 * 256 * 2 / 16, NM = kMLevels * 512 * 2 / 16;
     for (int i = t; i < NT + NM; i += kThreads) {
       if (i < NT) dT[i] = srcT[i];
       else dM[i - NT] = srcM[i - NT];
@@ -64,7 +84,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
     if (t < kMetaWords) S.meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
   }
   const uint16_t* M = &S.M[0][0];
-  const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform: scalar loads
+  const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
            __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -72,15 +92,22 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   const uint64_t F = rfl64(a.frame_off[g]);
   const uint64_t L = rfl64(a.frame_bytes[g]) - 2;  // = ceil(TB / 8): bytes covered by the CRC-16
   const int C = __builtin_amdgcn_readfirstlane(a.streams[a.frames[g].stream].channels);
+  uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
+#pragma unroll
+  for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = __builtin_amdgcn_readfirstlane(gmeta[kHdrWords + i]);
   __syncthreads();
   const uint32_t* hdrw = S.meta;
   const uint32_t* seg = S.meta + kHdrWords;
-  const uint32_t TB = seg[C + 1];               // frame bits before the byte pad
+  const uint32_t TB = sg[C + 1];                // frame bits before the byte pad
   const uint32_t A = (uint32_t)(F & 3);
   uint32_t* gw = (uint32_t*)(a.out + (F - A));  // dword k of this frame's span
   const int64_t ND = (int64_t)((F + L - 1) >> 2) - (int64_t)(F >> 2) + 1;  // dwords touching the frame
   const int64_t NF = (int64_t)((F + L) >> 2) - (int64_t)(F >> 2);          // dwords ending inside it
-  const int pad = (int)((kThreads - (NF % kThreads)) % kThreads);
+  const int a4 = (int)(((F - A) >> 2) & 3);
+  const int64_t NQ = (NF + a4 + 3) >> 2;       // quads holding CRC dwords
+  const int64_t NQW = (ND + a4 + 3) >> 2;      // quads holding output dwords (NQ or NQ + 1)
+  const int pad = (int)((kThreads - (NQ % kThreads)) % kThreads);
+  const int64_t kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
 
   // 32 frame bits starting at (possibly negative) bit position bp; bits outside [0, TB) read 0
@@ -105,35 +132,36 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
     return res;
   };
 
-  // Fast gather: a dword whose 32 bits lie inside ONE channel blob is a funnel shift of two adjacent
-  // slot words.  U dwords per thread are resolved and their loads issued together (latency overlap);
-  // dwords touching the header, a blob boundary or the frame ends take window() (a few per frame).
-  constexpr int U = 4;
-  uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
-#pragma unroll
-  for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = __builtin_amdgcn_readfirstlane(gmeta[kHdrWords + i]);
+  constexpr int U = 2;  // quads per thread per round
   uint32_t acc = 0;
-  int64_t k0 = (int64_t)t - pad;
-  if (k0 < 0) k0 += kThreads;
-  for (; k0 < ND; k0 += (int64_t)kThreads * U) {
-    uint32_t w0[U], w1[U], sh[U];
+  int64_t q0 = (int64_t)t - pad;  // quad index in v/4 space
+  if (q0 < 0) q0 += kThreads;
+  for (; q0 < NQW; q0 += (int64_t)kThreads * U) {
+    uint32_t w[U][5], sh[U];
     bool fast[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t k = k0 + (int64_t)u * kThreads;
+      const int64_t k = 4 * (q0 + (int64_t)u * kThreads) - a4;  // first dword of the quad
       const int64_t bp = 8 * (4 * k - (int64_t)A);
       fast[u] = false;
-      w0[u] = w1[u] = sh[u] = 0;
-      if (k < ND && bp >= (int64_t)sg[1] && bp + 32 <= (int64_t)TB) {
+      sh[u] = 0;
+#pragma unroll
+      for (int i = 0; i < 5; i++) w[u][i] = 0;
+      if (k >= 0 && k + 4 <= ND && bp >= (int64_t)sg[1] && bp + 128 <= (int64_t)TB) {
         const uint32_t b = (uint32_t)bp;
         int sgi = 1;  // blob sgi - 1 holds bit b: sg[sgi] <= b < sg[sgi + 1]
 #pragma unroll
         for (int i = 2; i <= kMaxChannels + 1; i++) sgi += (b >= sg[i]) ? 1 : 0;
-        if (b + 32 <= sg[sgi + 1]) {
+        if (b + 128 <= sg[sgi + 1]) {
           const uint32_t rel = b - sg[sgi];
           const uint32_t* src = slots + (size_t)(sgi - 1) * a.tmp_stride + (rel >> 5);
-          w0[u] = src[0];
-          w1[u] = src[1];
+          uint4 v4;
+          __builtin_memcpy(&v4, src, 16);
+          w[u][0] = v4.x;
+          w[u][1] = v4.y;
+          w[u][2] = v4.z;
+          w[u][3] = v4.w;
+          w[u][4] = src[4];
           sh[u] = rel & 31;
           fast[u] = true;
         }
@@ -141,39 +169,68 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t k = k0 + (int64_t)u * kThreads;
-      if (k >= ND) break;
-      const uint32_t val = fast[u] ? (uint32_t)((((uint64_t)w0[u] << 32) | w1[u]) >> (32 - sh[u]))
-                                   : window(8 * (4 * k - (int64_t)A));
-      if ((k > 0 || A == 0) && k < NF) {
-        gw[k] = __builtin_bswap32(val);
+      const int64_t q = q0 + (int64_t)u * kThreads;
+      if (q >= NQW) break;
+      const int64_t k = 4 * q - a4;
+      uint32_t val[4];
+      if (fast[u]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) val[i] = funnel(w[u][i], w[u][i + 1], sh[u]);
       } else {
-        for (int b = 0; b < 4; b++) {
-          const int64_t fb = 4 * k - (int64_t)A + b;  // frame byte index
-          if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val >> (24 - 8 * b));
+#pragma unroll
+        for (int i = 0; i < 4; i++) val[i] = (k + i >= 0 && k + i < ND) ? window(8 * (4 * (k + i) - (int64_t)A)) : 0u;
+      }
+      if (k >= kfull && k + 4 <= NF) {
+        uint4 o;
+        o.x = __builtin_bswap32(val[0]);
+        o.y = __builtin_bswap32(val[1]);
+        o.z = __builtin_bswap32(val[2]);
+        o.w = __builtin_bswap32(val[3]);
+        *reinterpret_cast<uint4*>(gw + k) = o;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int64_t kk = k + i;
+          if (kk < 0 || kk >= ND) continue;
+          if (kk >= kfull && kk < NF) {
+            gw[kk] = __builtin_bswap32(val[i]);
+          } else {
+            for (int b = 0; b < 4; b++) {
+              const int64_t fb = 4 * kk - (int64_t)A + b;  // frame byte index
+              if (fb >= 0 && fb < (int64_t)L) a.out[F + fb] = (uint8_t)(val[i] >> (24 - 8 * b));
+            }
+          }
+          if (kk == NF) S.tailw = val[i];
+          if (kk >= NF) val[i] = 0;  // trailing zeros in the CRC (removed below)
         }
       }
-      if (k == NF) S.tailw = val;
-      if (k < NF) {
-        const uint32_t c4 = (uint32_t)S.T[3][val >> 24] ^ (uint32_t)S.T[2][(val >> 16) & 0xFF] ^
-                            (uint32_t)S.T[1][(val >> 8) & 0xFF] ^ (uint32_t)S.T[0][val & 0xFF];
-        acc = crc_mul(M, 10, acc) ^ c4;  // Horner step: x^(32*256)
+      if (q < NQ) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          c ^= (uint32_t)S.T[15 - 4 * i][val[i] >> 24] ^ (uint32_t)S.T[14 - 4 * i][(val[i] >> 16) & 0xFF] ^
+               (uint32_t)S.T[13 - 4 * i][(val[i] >> 8) & 0xFF] ^ (uint32_t)S.T[12 - 4 * i][val[i] & 0xFF];
+        acc = crc_mul(M, 12, acc) ^ c;  // Horner step: x^(128*256)
       }
     }
   }
-  // combine: lane order == virtual dword order; left groups are multiplied by x^(32*2^l)
-  acc ^= crc_mul(M, 2, dpp32<DPP_SHR1, 0xF>(acc));
-  acc ^= crc_mul(M, 3, dpp32<DPP_SHR2, 0xF>(acc));
-  acc ^= crc_mul(M, 4, dpp32<DPP_SHR4, 0xF>(acc));
-  acc ^= crc_mul(M, 5, dpp32<DPP_SHR8, 0xF>(acc));
-  acc ^= crc_mul(M, 6, dpp32<DPP_BC15, 0xA>(acc));
-  acc ^= crc_mul(M, 7, dpp32<DPP_BC31, 0xC>(acc));
+  // combine: lane order == virtual quad order; left groups are multiplied by x^(128*2^l)
+  acc ^= crc_mul(M, 4, dpp32<DPP_SHR1, 0xF>(acc));
+  acc ^= crc_mul(M, 5, dpp32<DPP_SHR2, 0xF>(acc));
+  acc ^= crc_mul(M, 6, dpp32<DPP_SHR4, 0xF>(acc));
+  acc ^= crc_mul(M, 7, dpp32<DPP_SHR8, 0xF>(acc));
+  acc ^= crc_mul(M, 8, dpp32<DPP_BC15, 0xA>(acc));
+  acc ^= crc_mul(M, 9, dpp32<DPP_BC31, 0xC>(acc));
   if (lane == 63) S.crcw[wv] = acc;
   __syncthreads();
   if (t == 0) {
-    const uint32_t c01 = crc_mul(M, 8, S.crcw[0]) ^ S.crcw[1];
-    const uint32_t c23 = crc_mul(M, 8, S.crcw[2]) ^ S.crcw[3];
-    uint32_t crc = crc_mul(M, 9, c01) ^ c23;
+    const uint32_t c01 = crc_mul(M, 10, S.crcw[0]) ^ S.crcw[1];
+    const uint32_t c23 = crc_mul(M, 10, S.crcw[2]) ^ S.crcw[3];
+    uint32_t crc = crc_mul(M, 11, c01) ^ c23;
+    // remove the e zero dwords that followed dword NF-1 inside the last CRC quad: * x^(-32e)
+    const int e = (int)(4 * NQ - (NF + a4));
+    constexpr uint32_t kInvX32[4] = {0x0001u, 0xCAA8u, 0x25DDu, 0x37B1u};  // x^(-32e) mod P
+    if (e) crc = gf16_mul_dev(crc, kInvX32[e]);
     // tail: frame bytes [4*NF - A, L) not covered by whole dwords
     const int64_t tb0 = 4 * NF - (int64_t)A;
     if (tb0 < (int64_t)L) {
