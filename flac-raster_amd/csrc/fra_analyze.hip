@@ -450,6 +450,15 @@ read_x28(S.smp, t, x);
 #pragma unroll
     for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[t * kChunk + j];  // table padded by kMaxLpc
   }
+  // partial windows are zero outside their segment (host-computed extent [lo, hi)): a wave whose
+  // samples + lookahead [1024 wv, 1024 wv + 1024 + MAXLAG) miss it would only sum exact products of
+  // zeros, i.e. every chunk partial is +0.0 -- it skips the window and stores those zeros directly
+  auto wave_active = [&](const int wi) -> bool {
+    const int32_t* r = a.wrange + 2 * ((size_t)fr.win * a.nwin + wi);
+    const int lo = __builtin_amdgcn_readfirstlane(r[0]), hi = __builtin_amdgcn_readfirstlane(r[1]);
+    const int w0 = wv * 64 * kChunk;
+    return lo < w0 + 64 * kChunk + MAXLAG && hi > w0;
+  };
   // ---- 3. LPC analysis per apodization window (3.4-3.7)
   const int prec = qlp_precision(bps, n);
   if constexpr (MAXLAG > 0) {
@@ -461,7 +470,8 @@ read_x28(S.smp, t, x);
       // (window 0: FIXED searches on waves 1-3) + wave 0's Levinson-Durbin / order / quantisation.
       // Window 0 is peeled so its prefetched coefficients are dead after its first use (no live range
       // across the Levinson-Durbin section, which otherwise spills).
-      auto window_pass = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG]) {
+      auto window_pass = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG], const bool act) {
+        if (act) {
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];
@@ -496,6 +506,9 @@ read_x28(S.smp, t, x);
           }
         }
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi & 1][wv], lane);
+        } else if (lane <= MAXLAG) {
+          S.red[wi & 1][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
+        }
         __syncthreads();
         if (early && wi == 0 && (wv == 1 || wv == 2)) {  // the two FIXED candidates while wave 0 runs the LD
           int g1, g2;
@@ -557,13 +570,16 @@ read_x28(S.smp, t, x);
           }
         }
       };
-      window_pass(0, wcur);
+      window_pass(0, wcur, wave_active(0));
       for (int wi = 1; wi < a.nwin; wi++) {
         float wl[kChunk + MAXLAG];
+        const bool act = wave_active(wi);
         const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+        if (act) {
 #pragma unroll
-        for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
-        window_pass(wi, wl);
+          for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
+        }
+        window_pass(wi, wl, act);
       }
           } else {
         // levels 7-8 (up to 6 windows): every window's autocorrelation first, then Levinson-Durbin of
@@ -571,7 +587,11 @@ read_x28(S.smp, t, x);
       // 3.1 autocorrelation of every window: windowed samples -> chunk partials -> wave
       // reduce-scatter -> red[wi][wave][lag].  Window 0 is peeled so its prefetched coefficients die
       // at their first use.
-      auto window_acf = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG]) {
+      auto window_acf = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG], const bool act) {
+        if (!act) {
+          if (lane <= MAXLAG) S.red[wi][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
+          return;
+        }
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];
@@ -589,13 +609,7 @@ read_x28(S.smp, t, x);
         double acc[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++) acc[l] = 0.0;
-        // partial windows are zero outside their segment: a wave whose windowed samples are all zero
-        // keeps every partial at +0.0 (exact products of zeros sum to +0), so it skips the FMAs
-        bool nz = false;
-#pragma unroll
-        for (int j = 0; j < kChunk + MAXLAG; j++) nz |= wf[j] != 0.0f;
-        if (!__any(nz)) {
-        } else if (i0 + kChunk + MAXLAG <= n) {
+        if (i0 + kChunk + MAXLAG <= n) {
 #pragma unroll
           for (int jj = 0; jj < kChunk; jj++) {
             const double a0 = (double)wf[jj];
@@ -613,13 +627,16 @@ read_x28(S.smp, t, x);
         }
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi][wv], lane);
       };
-      window_acf(0, wcur);
+      window_acf(0, wcur, wave_active(0));
       for (int wi = 1; wi < a.nwin; wi++) {
         float wl[kChunk + MAXLAG];
+        const bool act = wave_active(wi);
         const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+        if (act) {
 #pragma unroll
-        for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
-        window_acf(wi, wl);
+          for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
+        }
+        window_acf(wi, wl, act);
       }
       __syncthreads();
       // 3.2 (fast 16-bit frames) the two FIXED candidates, searched on the two waves after the ones

@@ -83,6 +83,7 @@ struct fra_plan {
   FrameDev* d_frames = nullptr;
   NormDev* d_norm = nullptr;
   float* d_win = nullptr;
+  int32_t* d_wrange = nullptr;
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -241,6 +242,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_frames);
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_win);
+  (void)hipFree(p->d_wrange);
   (void)hipFree(p->d_sf);
   (void)hipFree(p->d_fbytes);
   (void)hipFree(p->d_foff);
@@ -370,6 +372,21 @@ static int plan_build(fra_plan* p) {
     window_set(wt.data() + t * std::max(1, p->nwin) * j.blocksize, win_sizes[t], j.blocksize, nsub);
   HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wt.size()));
   HIPCHK(hipMemcpy(p->d_win, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
+  {  // nonzero extent [lo, hi) of every window (k_analyze: waves outside it skip the autocorrelation)
+    const int nw = std::max(1, p->nwin), nt = (int)std::max<size_t>(1, win_sizes.size());
+    std::vector<int32_t> wr(2 * (size_t)nt * nw, 0);
+    for (int t = 0; t < nt; t++)
+      for (int w = 0; w < nw; w++) {
+        const float* o = wt.data() + ((size_t)t * nw + w) * j.blocksize;
+        int lo = j.blocksize, hi = 0;
+        for (int i = 0; i < j.blocksize; i++)
+          if (o[i] != 0.0f) { lo = std::min(lo, i); hi = i + 1; }
+        wr[2 * ((size_t)t * nw + w)] = lo < hi ? lo : 0;
+        wr[2 * ((size_t)t * nw + w) + 1] = lo < hi ? hi : 0;
+      }
+    HIPCHK(hipMalloc(&p->d_wrange, sizeof(int32_t) * wr.size()));
+    HIPCHK(hipMemcpy(p->d_wrange, wr.data(), sizeof(int32_t) * wr.size(), hipMemcpyHostToDevice));
+  }
   if (!p->streams.empty())
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
   if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
@@ -398,6 +415,7 @@ static int plan_build(fra_plan* p) {
   a.frames = p->d_frames;
   a.norm = p->d_norm;
   a.win = p->d_win;
+  a.wrange = p->d_wrange;
   a.sf = p->d_sf;
   a.frame_bytes = p->d_fbytes;
   a.frame_off = p->d_foff;
@@ -405,6 +423,7 @@ static int plan_build(fra_plan* p) {
   a.crctab = p->d_crctab;
   a.tmp = p->d_tmp;
   a.fmeta = p->d_fmeta;
+  a.out_cap = p->out_cap;
   a.tmp_stride = p->tmp_stride;
   a.lut = p->d_lut;
   a.lut_stride = lut_stride;

@@ -182,10 +182,12 @@ struct JobArgs {
   const FrameDev* frames;
   NormDev* norm;
   const float* win;        // [ntables][nwin][blocksize]
+  const int32_t* wrange;   // [ntables][nwin][2]: nonzero extent [lo, hi) of each window
   SfDesc* sf;              // [nframes_total][cmax]
   unsigned long long* frame_bytes;  // [nframes_total + 1] (last = 0)
   unsigned long long* frame_off;  // [nframes_total + 1] exclusive scan of frame_bytes
   uint8_t* out;            // concatenated frames
+  uint64_t out_cap;        // bytes allocated at out
   const uint16_t* crctab;  // CRC-16 slice-by-4 tables [4][256] + multiply-by-x^(8*2^i) tables [24][2][256]
   uint32_t* fmeta;         // [nframes_total][kMetaWords]: header (+CRC-8) as big-endian words, blob bit bounds
   uint32_t* tmp;           // encoded subframes: slot (frame*cmax + channel) of tmp_stride words

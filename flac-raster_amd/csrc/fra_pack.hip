@@ -26,6 +26,12 @@
 #include "fra_device.h"
 
 namespace fra {
+#ifdef FRA_GUARD
+__device__ int g_guard_count;
+#define GUARD(cond, ...) do { if (!(cond)) { if (atomicAdd(&g_guard_count, 1) < 40) printf(__VA_ARGS__); } } while (0)
+#else
+#define GUARD(cond, ...) do {} while (0)
+#endif
 
 constexpr int kMLo = 4, kMLevels = 9;  // LDS copy of multiply tables x^(8*2^i), i = 4..12
 
@@ -86,8 +92,8 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   const uint16_t* M = &S.M[0][0];
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);  // (readfirstlane is int: no sign extension)
   };
   const uint64_t F = rfl64(a.frame_off[g]);
   const uint64_t L = rfl64(a.frame_bytes[g]) - 2;  // = ceil(TB / 8): bytes covered by the CRC-16
@@ -109,6 +115,22 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   const int pad = (int)((kThreads - (NQ % kThreads)) % kThreads);
   const int64_t kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
+#ifdef FRA_GUARD
+  const uint64_t TOT = a.frame_off[a.nframes_total];
+  const uint64_t SLOTW = (uint64_t)a.nframes_total * a.cmax * a.tmp_stride;
+  {
+    const FrameDev frg = a.frames[g];
+    const StreamDev stg = a.streams[frg.stream];
+    const uint64_t cap = 18 + (uint64_t)C * ((uint64_t)frg.n * stg.bps / 8 + 8);
+    if (t == 0) GUARD(L + 2 <= cap, "g %d frame bytes %llu > cap %llu (n %d bps %d C %d) bits %u %u %u %u %u %u %u %u\n", g,
+                      (unsigned long long)(L + 2), (unsigned long long)cap, frg.n, stg.bps, C, sg[2] - sg[1], sg[3] - sg[2],
+                      sg[4] - sg[3], sg[5] - sg[4], sg[6] - sg[5], sg[7] - sg[6], sg[8] - sg[7], sg[9] - sg[8]);
+    const bool ok = (TB + 7) / 8 == L && F + L + 2 <= TOT && F + L + 2 <= a.out_cap && L + 2 <= cap && C >= 1 && C <= kMaxChannels;
+    if (t == 0) GUARD(ok, "g %d TB %u L %llu F %llu TOT %llu cap %llu C %d sg %u %u %u %u\n", g, TB, (unsigned long long)L,
+                      (unsigned long long)F, (unsigned long long)TOT, (unsigned long long)a.out_cap, C, sg[0], sg[1], sg[2], sg[C + 1]);
+    if (!ok) return;
+  }
+#endif
 
   // 32 frame bits starting at (possibly negative) bit position bp; bits outside [0, TB) read 0
   auto window = [&](int64_t bp) -> uint32_t {
@@ -155,6 +177,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
         if (b + 128 <= sg[sgi + 1]) {
           const uint32_t rel = b - sg[sgi];
           const uint32_t* src = slots + (size_t)(sgi - 1) * a.tmp_stride + (rel >> 5);
+          GUARD((uint64_t)(src + 4 - a.tmp) < SLOTW && sgi - 1 < C, "g %d slot read sgi %d rel %u\n", g, sgi, rel);
           uint4 v4;
           __builtin_memcpy(&v4, src, 16);
           w[u][0] = v4.x;
@@ -186,6 +209,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
         o.y = __builtin_bswap32(val[1]);
         o.z = __builtin_bswap32(val[2]);
         o.w = __builtin_bswap32(val[3]);
+        GUARD(F - A + 4 * k + 16 <= TOT, "g %d quad store k %lld\n", g, (long long)k);
         *reinterpret_cast<uint4*>(gw + k) = o;
       } else {
 #pragma unroll
