@@ -463,127 +463,6 @@ read_x28(S.smp, t, x);
   const int prec = qlp_precision(bps, n);
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
-      if constexpr (MAXLAG <= 8) {
-        // levels 3-6 (<= 3 windows): window by window, wave 0 runs Levinson-Durbin while waves 1-3
-        // run ahead (lowest register pressure: the 5-waves/SIMD configuration has no spills)
-      // one apodization window: windowed samples -> chunk partials -> wave reduce-scatter -> barrier ->
-      // (window 0: FIXED searches on waves 1-3) + wave 0's Levinson-Durbin / order / quantisation.
-      // Window 0 is peeled so its prefetched coefficients are dead after its first use (no live range
-      // across the Levinson-Durbin section, which otherwise spills).
-      auto window_pass = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG], const bool act) {
-        if (act) {
-        float wf[kChunk + MAXLAG];
-        {
-          int32_t y[kChunk + 8];
-          read_y24(S.smp, t, y);
-#pragma unroll
-          for (int j = 0; j < kChunk + MAXLAG; j++) {
-            const int i = i0 + j;
-            const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
-            wf[j] = (i < n) ? (float)v * wcoef[j] : 0.0f;
-          }
-        }
-
-        // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
-        // float*float product, so this is bit-identical to the oracle's acc + a*b
-        double acc[MAXLAG + 1];
-#pragma unroll
-        for (int l = 0; l <= MAXLAG; l++) acc[l] = 0.0;
-        if (i0 + kChunk + MAXLAG <= n) {
-#pragma unroll
-          for (int jj = 0; jj < kChunk; jj++) {
-            const double a0 = (double)wf[jj];
-#pragma unroll
-            for (int l = 0; l <= MAXLAG; l++) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
-          }
-        } else {
-#pragma unroll
-          for (int jj = 0; jj < kChunk; jj++) {
-            const double a0 = (double)wf[jj];
-#pragma unroll
-            for (int l = 0; l <= MAXLAG; l++)
-              if (i0 + jj + l < n) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
-          }
-        }
-        autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi & 1][wv], lane);
-        } else if (lane <= MAXLAG) {
-          S.red[wi & 1][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
-        }
-        __syncthreads();
-        if (early && wi == 0 && (wv == 1 || wv == 2)) {  // the two FIXED candidates while wave 0 runs the LD
-          int g1, g2;
-          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
-          if (wv == 1 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
-          const int m = wv == 1 ? g1 : g2;
-          if (m >= 0) {
-            const int pm = max_porder(n, m, cfg.max_porder);
-            uint64_t best = 0;
-            int bp = pm;
-            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
-            if (lane == 0) {
-              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
-              S.mporder[m] = bp;
-            }
-          }
-        }
-        // wave 0, uniformly: autocorrelation -> Levinson-Durbin (registers) -> expected bits of every
-        // order in parallel (lane o) -> first minimum -> qlp quantisation.  The other waves run ahead
-        // (next window / model-sum setup); red[] is double-buffered and the next barrier is only
-        // passed once wave 0 is done.
-        if (wv == 0) {
-          double ac[MAXLAG + 1];
-#pragma unroll
-          for (int l = 0; l <= MAXLAG; l++)
-            ac[l] = l <= lmax ? (S.red[wi & 1][0][l] + S.red[wi & 1][1][l]) + (S.red[wi & 1][2][l] + S.red[wi & 1][3][l])
-                              : 0.0;
-          const int m = 5 + wi;
-          int nord = 0;
-          double errv[MAXLAG];
-          if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[0], errv, lane == 0);
-          bool ok = false;
-          int o = 0, sh = 0;
-          int32_t q[MAXLAG];
-          if (nord > 0) {
-            double e = errv[0];
-#pragma unroll
-            for (int j = 1; j < MAXLAG; j++)
-              if (lane == j + 1) e = errv[j];
-            // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as
-            // an unsigned integer; DPP min over the wave, lowest lane among the equal ones
-            const bool on = lane >= 1 && lane <= nord;
-            const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lane, prec + sbps)) : ~0ull;
-            const uint64_t kmin = wave_min64(key);
-            o = (int)__builtin_ctzll(__ballot(on && key == kmin));
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's lp rows -> all lanes
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_wave_barrier();
-            double lpo[MAXLAG];
-#pragma unroll
-            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[0][o - 1][j];
-            ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
-          }
-          if (lane == 0) {
-            S.mvalid[m] = ok ? 1 : 0;
-            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
-#pragma unroll
-            for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
-          }
-        }
-      };
-      window_pass(0, wcur, wave_active(0));
-      for (int wi = 1; wi < a.nwin; wi++) {
-        float wl[kChunk + MAXLAG];
-        const bool act = wave_active(wi);
-        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
-        if (act) {
-#pragma unroll
-          for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
-        }
-        window_pass(wi, wl, act);
-      }
-          } else {
-        // levels 7-8 (up to 6 windows): every window's autocorrelation first, then Levinson-Durbin of
-        // window wi on wave wi % 4 in parallel
       // 3.1 autocorrelation of every window: windowed samples -> chunk partials -> wave
       // reduce-scatter -> red[wi][wave][lag].  Window 0 is peeled so its prefetched coefficients die
       // at their first use.
@@ -639,6 +518,77 @@ read_x28(S.smp, t, x);
         window_acf(wi, wl, act);
       }
       __syncthreads();
+      if constexpr (MAXLAG <= 8) {
+        // levels 3-6 (<= 3 windows): the two FIXED candidates on waves 1-2 while wave 0 runs the
+        // Levinson-Durbin of EVERY window at once, window w on lanes 16w..16w+15 (the same op sequence
+        // per lane: one window's instruction cost for all three) -> expected bits of order o on lane
+        // 16w+o -> first minimum per lane group -> qlp quantisation per group
+        if (early && (wv == 1 || wv == 2)) {
+          int g1, g2;
+          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
+          if (wv == 1 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
+          const int m = wv == 1 ? g1 : g2;
+          if (m >= 0) {
+            const int pm = max_porder(n, m, cfg.max_porder);
+            uint64_t best = 0;
+            int bp = pm;
+            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
+            if (lane == 0) {
+              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
+              S.mporder[m] = bp;
+            }
+          }
+        }
+        if (wv == 0) {
+          const int gw = lane >> 4, lo = lane & 15;
+          const bool gon = gw < a.nwin;
+          const int ws = gon ? gw : 0;
+          double ac[MAXLAG + 1];
+#pragma unroll
+          for (int l = 0; l <= MAXLAG; l++)
+            ac[l] = l <= lmax ? (S.red[ws][0][l] + S.red[ws][1][l]) + (S.red[ws][2][l] + S.red[ws][3][l]) : 0.0;
+          int nord = 0;
+          double errv[MAXLAG];
+          if (gon && ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[ws], errv, lo == 0);
+          double e = errv[0];
+#pragma unroll
+          for (int j = 1; j < MAXLAG; j++)
+            if (lo == j + 1) e = errv[j];
+          // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as an
+          // unsigned integer; DPP min inside each 16-lane row (lane 15 of the row), lowest lane among
+          // the equal ones
+          const bool on = nord > 0 && lo >= 1 && lo <= nord;
+          const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lo, prec + sbps)) : ~0ull;
+          uint64_t rk = min(key, dpp64_old<DPP_SHR1, 0xF>(key, ~0ull));
+          rk = min(rk, dpp64_old<DPP_SHR2, 0xF>(rk, ~0ull));
+          rk = min(rk, dpp64_old<DPP_SHR4, 0xF>(rk, ~0ull));
+          rk = min(rk, dpp64_old<DPP_SHR8, 0xF>(rk, ~0ull));
+          const uint64_t kmin = __shfl(rk, (lane & 48) | 15, 64);
+          const uint64_t bal = __ballot(on && key == kmin);
+          const uint32_t rowbits = (uint32_t)(bal >> (16 * gw)) & 0xFFFFu;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // group leaders' lp rows -> all lanes
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_wave_barrier();
+          bool ok = false;
+          int o = 0, sh = 0;
+          int32_t q[MAXLAG];
+          if (nord > 0) {
+            o = (int)__builtin_ctz(rowbits);
+            double lpo[MAXLAG];
+#pragma unroll
+            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[ws][o - 1][j];
+            ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
+          }
+          if (gon && lo == 0) {
+            const int m = 5 + gw;
+            S.mvalid[m] = ok ? 1 : 0;
+            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
+#pragma unroll
+            for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
+          }
+        }
+      } else {
+        // levels 7-8 (up to 6 windows): Levinson-Durbin of window wi on wave wi % 4 in parallel
       // 3.2 (fast 16-bit frames) the two FIXED candidates, searched on the two waves after the ones
       // running Levinson-Durbin (psum is complete since the barrier above)
       if (early) {
@@ -811,6 +761,7 @@ read_x28(S.smp, t, x);
     }
   }
   __syncthreads();
+  FRA_STOP(5)
   if constexpr (!B32) {
     if (fastframe) {
       // ---- 6+7, fast 16-bit frames: every wave derives the winner and the partition Rice parameters
@@ -886,6 +837,7 @@ read_x28(S.smp, t, x);
         atomicAdd(&S.esum2[pidx][2], (unsigned long long)fs2);
       }
       __syncthreads();
+      FRA_STOP(6)
       // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
       const int npp = 1 << ps;
       const int k0j = __shfl(kl, lane < npp ? ((lane + 1) << smax) - 1 : 0, 64);
@@ -937,6 +889,7 @@ read_x28(S.smp, t, x);
       const uint32_t inc = wave_incl_scan32(tot);
       if (lane == 63) S.scan[wv] = inc;
       __syncthreads();
+      FRA_STOP(7)
       const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
       if (t == 0) {
         const int tcode = verbatim ? 1 : type == 2 ? 8 + o : 31 + o;
