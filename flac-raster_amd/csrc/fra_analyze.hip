@@ -483,27 +483,25 @@ read_x28(S.smp, t, x);
           }
         }
 
-        // chunk partials (FRA-1): per lag sequential over the 16 samples; fma == add of the exact
-        // float*float product, so this is bit-identical to the oracle's acc + a*b
-        double acc[MAXLAG + 1];
+        // chunk partials (FRA-1): per lag, the even and the odd samples of the chunk are summed
+        // separately in float (fused multiply-add, ascending), then ae + ao in float, widened to double
+        // -- one v_pk_fma_f32 per (sample pair, lag).  Samples at or past n are 0.0f, whose products
+        // leave a float sum unchanged, so no tail masking is needed (= the oracle's skipped terms).
+        f32x2 pacc[MAXLAG + 1];
 #pragma unroll
-        for (int l = 0; l <= MAXLAG; l++) acc[l] = 0.0;
-        if (i0 + kChunk + MAXLAG <= n) {
+        for (int l = 0; l <= MAXLAG; l++) pacc[l] = f32x2{0.0f, 0.0f};
 #pragma unroll
-          for (int jj = 0; jj < kChunk; jj++) {
-            const double a0 = (double)wf[jj];
+        for (int pp = 0; pp < kChunk / 2; pp++) {
+          const f32x2 a2 = {wf[2 * pp], wf[2 * pp + 1]};
 #pragma unroll
-            for (int l = 0; l <= MAXLAG; l++) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
-          }
-        } else {
-#pragma unroll
-          for (int jj = 0; jj < kChunk; jj++) {
-            const double a0 = (double)wf[jj];
-#pragma unroll
-            for (int l = 0; l <= MAXLAG; l++)
-              if (i0 + jj + l < n) acc[l] = fma(a0, (double)wf[jj + l], acc[l]);
+          for (int l = 0; l <= MAXLAG; l++) {
+            const f32x2 b2 = {wf[2 * pp + l], wf[2 * pp + l + 1]};
+            pacc[l] = __builtin_elementwise_fma(a2, b2, pacc[l]);
           }
         }
+        double acc[MAXLAG + 1];
+#pragma unroll
+        for (int l = 0; l <= MAXLAG; l++) acc[l] = (double)(pacc[l].x + pacc[l].y);
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi][wv], lane);
       };
       window_acf(0, wcur, wave_active(0));

@@ -103,6 +103,8 @@ template <> struct RawType<ST_U32> { using T = uint32_t; };
 template <> struct RawType<ST_I32> { using T = int32_t; };
 template <> struct RawType<ST_F32> { using T = float; };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <typename T, int V>
 struct alignas(sizeof(T) * V) VecT {
   T v[V];

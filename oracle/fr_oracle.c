@@ -232,8 +232,7 @@ ORA_API void ora_window_set(float *w /* nwin*N */, int N, int nsub) {
 
 /* ================================================================== analysis primitives */
 
-/* Autocorrelation, FRA-1 fixed reduction order: 16-sample chunks summed sequentially
- * (acc starts at +0.0, products of two floats are exact in double), 256 chunk partials
+/* Autocorrelation, FRA-1 fixed reduction order: 16-sample chunks (float partials, below), 256 chunk partials
  * (zero padded); each group of 64 (one GPU wave) reduced by a pairwise tree with DESCENDING
  * strides 32,16,...,1 (P[j] = P[j] + P[j+s], j < s inside the group), then the four group
  * sums as (G0 + G1) + (G2 + G3). */
@@ -241,11 +240,14 @@ ORA_API void ora_autocorr(const float *wf, int n, int maxlag, double *autoc) {
   double P[256];
   for (int l = 0; l <= maxlag; l++) {
     for (int j = 0; j < 256; j++) {
-      double acc = 0.0;
-      for (int i = 16 * j; i < 16 * j + 16; i++) {
-        if (i + l < n) acc = acc + (double)wf[i] * (double)wf[i + l];
+      /* chunk partial: even and odd samples summed separately in float by fused multiply-add,
+       * then ae + ao in float (k_analyze: one v_pk_fma_f32 per sample pair and lag) */
+      float ae = 0.0f, ao = 0.0f;
+      for (int i = 16 * j; i < 16 * j + 16; i += 2) {
+        if (i + l < n) ae = fmaf(wf[i], wf[i + l], ae);
+        if (i + 1 + l < n) ao = fmaf(wf[i + 1], wf[i + 1 + l], ao);
       }
-      P[j] = acc;
+      P[j] = (double)(ae + ao);
     }
     for (int g = 0; g < 256; g += 64)
       for (int s = 32; s >= 1; s >>= 1)
