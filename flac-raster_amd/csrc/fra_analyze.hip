@@ -97,20 +97,22 @@ struct AnalyzeSmem {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
     uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
   } u;
-  unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
-  unsigned long long esum2[kMaxPart][3];     // fast frames: exact-pass sums of u >> (k0-1), u >> k0, u >> (k0+1)
+  union {
+    unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
+    struct {  // after the model search (node is dead): winner's exact-pass sums / Rice parameters
+      unsigned long long esum2[kMaxPart][3];  // fast frames: sums of u >> (k0-1), u >> k0, u >> (k0+1)
+      int32_t kpart[kMaxPart];
+      int32_t kfin[kMaxPart];
+    } e;
+  } nu;
   double red[kWinCap<MAXLAG>()][4][MAXLAG + 1];  // per window, per wave: reduced chunk partials
-  double autoc[kMaxLpc + 1];
   double lp[kLdWaves<MAXLAG>()][MAXLAG > 0 ? MAXLAG : 1][MAXLAG > 0 ? MAXLAG : 1];  // LD rows per LD wave
-  double err[kMaxLpc];
   int32_t mcoef[kMaxModels][kMaxLpc];
   int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
   uint32_t ired[4][3];
-  int32_t kpart[kMaxPart];
-  int32_t kfin[kMaxPart];
   uint32_t scan[4];
-  int32_t nord, olo, ohi, winner, ftype, fmethod;
+  int32_t winner, ftype, fmethod;
   uint32_t fbits;
 };
 
@@ -316,7 +318,7 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
 }
 
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : 5) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -349,7 +351,6 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : 5) k_analyze(JobArgs a, in
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
-  for (int i = t; i < kMaxPart * 3; i += kThreads) (&S.esum2[0][0])[i] = 0ull;
   orv = wave_or32(orv);
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys
   const uint32_t kmax = ~wave_min32(~((uint32_t)vmax ^ 0x80000000u));
@@ -530,7 +531,7 @@ read_x28(S.smp, t, x);
             const int pm = max_porder(n, m, cfg.max_porder);
             uint64_t best = 0;
             int bp = pm;
-            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
+            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp);
             if (lane == 0) {
               S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
               S.mporder[m] = bp;
@@ -600,7 +601,7 @@ read_x28(S.smp, t, x);
             const int pm = max_porder(n, m, cfg.max_porder);
             uint64_t best = 0;
             int bp = pm;
-            porder_search(S.u.psum[m], S.node[wv], P, pm, n, m, lane, best, bp);
+            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp);
             if (lane == 0) {
               S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
               S.mporder[m] = bp;
@@ -752,11 +753,17 @@ read_x28(S.smp, t, x);
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], S.node[wv], P, pm, n, o, lane, best, bp);
+    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
     }
+  }
+  {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share
+    static_assert(kMaxPart * 3 <= 2 * (2 * kMaxPart), "esum2 inside node[0..1]");
+    unsigned long long* ez = &S.nu.e.esum2[0][0];
+    const int e1 = min(kMaxPart * 3, (wv + 1) * 2 * kMaxPart);
+    for (int i = wv * 2 * kMaxPart + lane; i < e1; i += 64) ez[i] = 0ull;
   }
   __syncthreads();
   FRA_STOP(5)
@@ -830,9 +837,9 @@ read_x28(S.smp, t, x);
         }
       }
       if (live) {
-        atomicAdd(&S.esum2[pidx][0], (unsigned long long)fs0);
-        atomicAdd(&S.esum2[pidx][1], (unsigned long long)fs1);
-        atomicAdd(&S.esum2[pidx][2], (unsigned long long)fs2);
+        atomicAdd(&S.nu.e.esum2[pidx][0], (unsigned long long)fs0);
+        atomicAdd(&S.nu.e.esum2[pidx][1], (unsigned long long)fs1);
+        atomicAdd(&S.nu.e.esum2[pidx][2], (unsigned long long)fs2);
       }
       __syncthreads();
       FRA_STOP(6)
@@ -846,7 +853,7 @@ read_x28(S.smp, t, x);
         bool first = true;
         for (int kk = k0j - 1; kk <= k0j + 1; kk++) {
           if (kk < 0 || kk > 30) continue;
-          const uint64_t e = cnt * (uint64_t)(kk + 1) + S.esum2[lane][kk - k0j + 1];
+          const uint64_t e = cnt * (uint64_t)(kk + 1) + S.nu.e.esum2[lane][kk - k0j + 1];
           if (first || e < best) { best = e; bk = kk; first = false; }
         }
       }
@@ -955,7 +962,7 @@ read_x28(S.smp, t, x);
       int k;
       uint64_t bits;
       rice_pick(cnt, Sv, k, bits);
-      S.kpart[j] = k;
+      S.nu.e.kpart[j] = k;
     }
   }
   __syncthreads();
@@ -1015,7 +1022,7 @@ read_x28(S.smp, t, x);
     uint64_t e0 = 0, e1 = 0, e2 = 0;
     if (fastframe) {
       const int pidx = i0 < n ? i0 / pz : 0;
-      const int k = S.kpart[pidx];
+      const int k = S.nu.e.kpart[pidx];
       const int km = k > 0 ? k - 1 : 0;  // e0 is only used when k >= 1
       if constexpr (B32) {
 #pragma unroll
@@ -1042,7 +1049,7 @@ read_x28(S.smp, t, x);
       }
     } else if (i0 < n) {
       int pidx = i0 / pz, pend = (pidx + 1) * pz;
-      int k = S.kpart[pidx];
+      int k = S.nu.e.kpart[pidx];
       const int iend = min(i0 + kChunk, n);
       for (int i = max(i0, o); i < iend; i++) {
         if (i >= pend) {
@@ -1052,7 +1059,7 @@ read_x28(S.smp, t, x);
           e0 = e1 = e2 = 0;
           pidx = i / pz;
           pend = (pidx + 1) * pz;
-          k = S.kpart[pidx];
+          k = S.nu.e.kpart[pidx];
         }
         uint32_t u = 0;
 #pragma unroll
@@ -1074,7 +1081,7 @@ read_x28(S.smp, t, x);
     int bk = 0;
     if (lane < npp) {
       const uint64_t cnt = (uint64_t)((n >> ps) - (lane == 0 ? o : 0));
-      const int k0 = S.kpart[lane];
+      const int k0 = S.nu.e.kpart[lane];
       bool first = true;
       for (int kk = k0 - 1; kk <= k0 + 1; kk++) {
         if (kk < 0 || kk > 30) continue;
@@ -1086,7 +1093,7 @@ read_x28(S.smp, t, x);
     const uint64_t tot = (uint64_t)wave_sum32(lane < npp ? (uint32_t)best : 0u) + (uint64_t)npp * (big ? 5 : 4) + 6;
     const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + tot;
     const bool verbatim = exact >= verb;
-    if (lane < npp) { d->k[lane] = (uint8_t)bk; S.kfin[lane] = bk; }
+    if (lane < npp) { d->k[lane] = (uint8_t)bk; S.nu.e.kfin[lane] = bk; }
     if (lane < kMaxLpc) d->coef[lane] = type == 3 ? S.mcoef[m][lane] : 0;
     if (lane == 0) {
       d->wasted = (uint8_t)w;
@@ -1142,8 +1149,8 @@ read_x28(S.smp, t, x);
       // sums (kcur is k0-1, k0 or k0+1), the partition parameter in front of the thread's first code
       const bool live = i0 < n;
       const int pidx = live ? i0 / pz : 0;
-      const int kcur = S.kfin[pidx];
-      const int dk = kcur - S.kpart[pidx];
+      const int kcur = S.nu.e.kfin[pidx];
+      const int dk = kcur - S.nu.e.kpart[pidx];
       const bool pstart = live && i0 == pidx * pz;
       const uint32_t cnt = live ? (uint32_t)(kChunk - (head ? o : 0)) : 0u;
       const uint32_t tot = live ? (dk < 0 ? fs[0] : dk == 0 ? fs[1] : fs[2]) + cnt * (uint32_t)(kcur + 1) +
@@ -1168,13 +1175,13 @@ read_x28(S.smp, t, x);
     uint32_t kk[kChunk];  // Rice parameter | partition-start << 8, 0xFFFF = no code
     uint32_t tot = 0;
     int pidx = i0 < n ? i0 / pz : 0, pend = (pidx + 1) * pz;
-    int kcur = S.kfin[pidx];
+    int kcur = S.nu.e.kfin[pidx];
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) {
       const int i = i0 + jj;
       kk[jj] = 0xFFFFu;
       if (i < n && i >= o) {
-        if (i >= pend) { pidx++; pend += pz; kcur = S.kfin[pidx]; }
+        if (i >= pend) { pidx++; pend += pz; kcur = S.nu.e.kfin[pidx]; }
         const bool pstart = (pidx == 0) ? (i == o) : (i == pidx * pz);
         kk[jj] = (uint32_t)kcur | (pstart ? 0x100u : 0u);
         tot += (uu[jj] >> kcur) + 1u + (uint32_t)kcur + (pstart ? (uint32_t)pb : 0u);
