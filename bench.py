@@ -253,7 +253,7 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "u16->i16 (int32 analysis, f64 autocorr)" if cfg["norm"] == 16 else "f32->i32 (int64 analysis)",
+            "dtype": "u16->i16 (int32 analysis, f32 chunk partials + f64 autocorr tree)" if cfg["norm"] == 16 else "f32->i32 (int64 analysis)",
             "data": "synthetic (flac_raster.synth, seed 20260227; device-generated, integer-exact numpy mirror)",
             "config": {"workload": cfg["workload"], "level": cfg["level"], "tiles": len(wins),
                        "raster_bytes": raster_bytes, "compressed_bytes": int(out_bytes_all),
