@@ -162,18 +162,23 @@ def main():
     for _ in range(args.warmup):
         plan.execute()
     plan.sync()
-    plan.enable_timing(True)
     barrier()
     plan.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.execute()
+        plan.execute()  # frame groups pipelined over streams
     plan.sync()
     t1 = time.perf_counter()
     barrier()
     dt_s = t1 - t0
     T = allmax(dt_s)
+    # per-kernel launch times (roofline): the same steps again, serial, HIP events between kernels
+    plan.enable_timing(True)
+    for _ in range(args.steps):
+        plan.execute()
+    plan.sync()
     kms, nexec = plan.timing()
+    plan.enable_timing(False)
     infos, total = plan.result()
     my_px = sum(w[2] * w[3] for w in my_wins)
     my_in_bytes = my_px * B * dt.itemsize
@@ -260,7 +265,9 @@ def main():
                        "compression_ratio": round(raster_bytes * (world if weak else 1) / max(1.0, out_bytes_all), 4),
                        "msamples_per_s": round(job_px * B * args.steps / T / 1e6, 1),
                        "parallelism": (f"{world} scene(s), one per GPU, no collective" if weak else
-                                       f"one scene's tiles sharded LPT over {world} GPU(s), no collective")},
+                                       f"one scene's tiles sharded LPT over {world} GPU(s), no collective"),
+                       "frame_groups": int(os.environ.get("FRA_GROUPS", "1")),
+                       "serial_ms_per_step": round(step_ms_local, 4)},
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "alg_bytes_per_launch": int(alg_bytes),

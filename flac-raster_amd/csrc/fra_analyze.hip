@@ -321,7 +321,7 @@ template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  const int g = blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = a.frame_base + (int)blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   if (c >= st.channels) return;
@@ -836,7 +836,25 @@ read_x28(S.smp, t, x);
           fs2 += uu[jj] >> (k0 + 1);
         }
       }
-      if (live) {
+      const int tpp = pz >> 4;  // threads per partition (uniform)
+      if ((tpp & (tpp - 1)) == 0) {
+        // partitions cover aligned groups of tpp lanes: reduce each group's (<= 64 lanes) sums on the
+        // upper-lane tree first, then one LDS atomic per partition and wave from the group's last lane
+        // (same-address atomics of up to 64 lanes would serialise).  n is a multiple of pz, so a group
+        // is entirely live or entirely past n.
+        const int ls = min(6, 31 - __builtin_clz((uint32_t)tpp));
+        uint64_t v0 = fs0, v1 = fs1, v2 = fs2;
+#define FRA_UP(S_)                                                                     \
+        if (ls > S_) { v0 = up_add64<S_>(v0); v1 = up_add64<S_>(v1); v2 = up_add64<S_>(v2); }
+        FRA_UP(0) FRA_UP(1) FRA_UP(2) FRA_UP(3) FRA_UP(4) FRA_UP(5)
+#undef FRA_UP
+        const int gm = (1 << ls) - 1;
+        if (live && (lane & gm) == gm) {
+          atomicAdd(&S.nu.e.esum2[pidx][0], (unsigned long long)v0);
+          atomicAdd(&S.nu.e.esum2[pidx][1], (unsigned long long)v1);
+          atomicAdd(&S.nu.e.esum2[pidx][2], (unsigned long long)v2);
+        }
+      } else if (live) {
         atomicAdd(&S.nu.e.esum2[pidx][0], (unsigned long long)fs0);
         atomicAdd(&S.nu.e.esum2[pidx][1], (unsigned long long)fs1);
         atomicAdd(&S.nu.e.esum2[pidx][2], (unsigned long long)fs2);
@@ -1210,7 +1228,8 @@ read_x28(S.smp, t, x);
 }
 
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s) {
-  dim3 grid((unsigned)a.nframes_total, (unsigned)a.cmax);
+  if (a.frame_count <= 0) return hipSuccess;
+  dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
 #define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)

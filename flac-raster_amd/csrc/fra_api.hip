@@ -6,8 +6,9 @@
 // (graph-capturable).  Per-job launch sequence (fra_kernels.hip):
 //   k_norm_init, k_minmax, k_norm_finalize  (skipped when norm == 0)
 //   k_analyze  [frames x channels]
-//   k_frame_bytes + hipcub exclusive scan
-//   k_pack     [frames]
+//   k_frame_bytes + hipcub exclusive scan + k_group_offsets
+//   k_assemble [frames]
+// Large plans run as FRA_GROUPS frame groups on their own streams (fra_plan_execute).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -33,6 +34,9 @@ hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t 
 hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
+hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
+                                unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
+                                hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int bands, int H, int W, void* out, hipStream_t s);
 hipError_t launch_normalize_flat(int src, const void* data, uint64_t n, int bps, NormDev* nd, int has_min, double omin,
                                  int has_max, double omax, void* out, hipStream_t s);
@@ -97,6 +101,15 @@ struct fra_plan {
   int32_t* d_lut = nullptr;
   int64_t tmp_stride = 0;
   JobArgs args{};
+  // frame groups: contiguous window runs [w0, w1) with frames [f0, f1).  Group g > 0 runs on aux[g - 1]
+  // (group 0 on the context stream) so one group's minmax/assemble overlaps another's k_analyze.
+  struct Group { int w0, w1, f0, f1; };
+  std::vector<Group> groups;            // pipelined execution (size 1 = serial)
+  Group all{0, 0, 0, 0};                // the whole plan as one group (timing mode)
+  std::vector<hipStream_t> aux;
+  std::vector<hipEvent_t> gev;          // [0] start, then per group: offsets-published, done
+  unsigned long long* d_gbase = nullptr;  // [groups + 1] byte offset of each group's first frame
+  size_t scan_stride = 0;               // bytes of scan workspace per group
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -252,6 +265,11 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_tmp);
   (void)hipFree(p->d_fmeta);
   (void)hipFree(p->d_lut);
+  (void)hipFree(p->d_gbase);
+  for (auto& st : p->aux)
+    if (st) (void)hipStreamDestroy(st);
+  for (auto& e : p->gev)
+    if (e) (void)hipEventDestroy(e);
   for (auto& e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;
@@ -391,9 +409,49 @@ static int plan_build(fra_plan* p) {
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
   if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(p->d_norm, 0, sizeof(NormDev) * std::max<size_t>(1, p->streams.size())));
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, p->scan_tmp_bytes, p->d_fbytes, p->d_foff, nfr + 1,
-                                          p->ctx->stream));
-  HIPCHK(hipMalloc(&p->d_scan_tmp, std::max<size_t>(16, p->scan_tmp_bytes)));
+  // frame groups: FRA_GROUPS (default 1: measured no gain on C4) contiguous window runs of about equal frame count;
+  // one group for small plans, where launch latency dominates
+  {
+    int G = 1;
+    if (const char* ev = getenv("FRA_GROUPS")) G = std::max(1, std::min(8, atoi(ev)));
+    if (nfr < 4096) G = 1;
+    p->all = {0, (int)p->streams.size(), 0, nfr};
+    p->groups.clear();
+    int w = 0, f = 0;
+    for (int g = 0; g < G && w < (int)p->streams.size(); g++) {
+      const int64_t target = (int64_t)nfr * (g + 1) / G;
+      fra_plan::Group gr{w, w, f, f};
+      while (w < (int)p->streams.size() && (g == G - 1 || f < target || gr.f1 == gr.f0)) {
+        f += p->streams[w].nframes;
+        w++;
+        gr.w1 = w;
+        gr.f1 = f;
+      }
+      p->groups.push_back(gr);
+    }
+    if (p->groups.empty()) p->groups.push_back(p->all);
+    p->groups.back().w1 = (int)p->streams.size();
+    p->groups.back().f1 = nfr;
+    size_t mx = 0, tb = 0;
+    for (const auto& gr : p->groups) {
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->d_fbytes, p->d_foff, std::max(1, gr.f1 - gr.f0),
+                                              p->ctx->stream));
+      mx = std::max(mx, tb);
+    }
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->d_fbytes, p->d_foff, std::max(1, nfr), p->ctx->stream));
+    mx = std::max(mx, tb);
+    p->scan_stride = (std::max<size_t>(16, mx) + 255) & ~(size_t)255;
+    p->scan_tmp_bytes = p->scan_stride * p->groups.size();
+    HIPCHK(hipMalloc(&p->d_scan_tmp, p->scan_tmp_bytes));
+    HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) * (p->groups.size() + 1)));
+    for (size_t g = 1; g < p->groups.size(); g++) {
+      hipStream_t st = nullptr;
+      HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      p->aux.push_back(st);
+    }
+    p->gev.assign(1 + 2 * p->groups.size(), nullptr);
+    for (auto& e : p->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   // per-subframe slots for the encoded subframes (k_analyze -> k_assemble)
   p->tmp_stride = ((int64_t)j.blocksize * bps + 64 + 31) / 32 + 4;
   HIPCHK(hipMalloc(&p->d_tmp, sizeof(uint32_t) * (size_t)p->tmp_stride * std::max(1, nfr) * p->cmax));
@@ -498,6 +556,43 @@ static void collect_times(fra_plan* p) {
   p->pending_times = false;
 }
 
+// one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
+// global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
+static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
+                     hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan) {
+  const JobArgs& a = p->args;
+  const int nst = gr.w1 - gr.w0, nf = gr.f1 - gr.f0;
+  if (p->job.norm != 0 && nst > 0 && p->max_segs > 0) {
+    JobArgs ma = a;  // the minmax family indexes streams by blockIdx.y: offset to the group's windows
+    ma.streams += gr.w0;
+    ma.norm += gr.w0;
+    if (ma.lut) ma.lut += (int64_t)gr.w0 * a.lut_stride;
+    const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
+    HIPCHK(launch_minmax(p->src, ma, nst, p->max_segs, vec, p->mm_rows, p->mm_max_rows, st));
+    HIPCHK(launch_norm_finalize(ma, nst, st));
+    HIPCHK(launch_norm_lut(p->src, ma, nst, st));
+  }
+  if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
+  JobArgs ga = a;
+  ga.frame_base = gr.f0;
+  ga.frame_count = nf;
+  HIPCHK(launch_analyze(p->src, p->b32, ga, st));
+  if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
+  HIPCHK(launch_frame_bytes(ga, st));
+  if (nf > 0) {
+    size_t tb = p->scan_stride;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)gi * p->scan_stride, tb,
+                                            p->d_fbytes + gr.f0, p->d_foff + gr.f0, nf, st));
+  }
+  if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
+  HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
+                              a.nframes_total, st));
+  if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
+  if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
+  HIPCHK(launch_assemble(ga, st));
+  return FRA_OK;
+}
+
 int fra_plan_execute(fra_plan* p) {
   if (!p) return set_err(FRA_E_INVALID, "null plan");
   if (!p->d_raster && !p->streams.empty()) return set_err(FRA_E_STATE, "plan has no raster");
@@ -505,26 +600,30 @@ int fra_plan_execute(fra_plan* p) {
   hipStream_t s = p->ctx->stream;
   if (p->timing) collect_times(p);
   p->args.vec8 = (p->ld_vec8 && (uintptr_t)p->d_raster % 8 == 0) ? 1 : 0;
-  const JobArgs& a = p->args;
-  const int nstreams = (int)p->streams.size();
-  if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));
-  if (p->job.norm != 0 && nstreams > 0 && p->max_segs > 0) {
-    const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
-    HIPCHK(launch_minmax(p->src, a, nstreams, p->max_segs, vec, p->mm_rows, p->mm_max_rows, s));
-    HIPCHK(launch_norm_finalize(a, nstreams, s));
-    HIPCHK(launch_norm_lut(p->src, a, nstreams, s));
-  }
-  if (p->timing) HIPCHK(hipEventRecord(p->ev[1], s));
-  if (a.nframes_total > 0) HIPCHK(launch_analyze(p->src, p->b32, a, s));
-  if (p->timing) HIPCHK(hipEventRecord(p->ev[2], s));
-  HIPCHK(launch_frame_bytes(a, s));
-  size_t tb = p->scan_tmp_bytes;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(p->d_scan_tmp, tb, p->d_fbytes, p->d_foff, a.nframes_total + 1, s));
-  if (p->timing) HIPCHK(hipEventRecord(p->ev[3], s));
-  HIPCHK(launch_assemble(a, s));
-  if (p->timing) {
-    HIPCHK(hipEventRecord(p->ev[4], s));
-    p->pending_times = true;
+  int rc = FRA_OK;
+  if (p->timing || p->groups.size() == 1) {
+    // serial: the whole plan as one group; timing events bracket each kernel phase
+    if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));
+    hipEvent_t* e = p->ev;
+    rc = run_group(p, p->timing ? p->all : p->groups[0], 0, 1, s, nullptr, nullptr, p->timing ? e[1] : nullptr,
+                   p->timing ? e[2] : nullptr, p->timing ? e[3] : nullptr);
+    if (rc) return rc;
+    if (p->timing) {
+      HIPCHK(hipEventRecord(p->ev[4], s));
+      p->pending_times = true;
+    }
+  } else {
+    const int ng = (int)p->groups.size();
+    HIPCHK(hipEventRecord(p->gev[0], s));
+    for (int g = 1; g < ng; g++) HIPCHK(hipStreamWaitEvent(p->aux[g - 1], p->gev[0], 0));
+    for (int g = 0; g < ng; g++) {
+      hipStream_t st = g == 0 ? s : p->aux[g - 1];
+      rc = run_group(p, p->groups[g], g, ng, st, g ? p->gev[1 + 2 * (g - 1)] : nullptr, p->gev[1 + 2 * g], nullptr,
+                     nullptr, nullptr);
+      if (rc) return rc;
+      if (g) HIPCHK(hipEventRecord(p->gev[2 + 2 * g], st));
+    }
+    for (int g = 1; g < ng; g++) HIPCHK(hipStreamWaitEvent(s, p->gev[2 + 2 * g], 0));
   }
   p->executed = true;
   return FRA_OK;

@@ -200,6 +200,8 @@ struct JobArgs {
   int32_t level;
   int32_t nwin;
   int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
+  int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
+  int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
 };
 
 }  // namespace fra

@@ -121,8 +121,9 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
   const int nr = min(st.height - r0, rows);
   const uint32_t nv = (uint32_t)(st.width / V);
   const uint32_t E = (uint32_t)nr * nv;  // (row, vector) items per band
-  // idx / nv by multiply-high: exact while E * nv < 2^32 (checked on the host)
-  const uint32_t magic = 0xFFFFFFFFu / nv + 1u;
+  // idx / nv by multiply-high: exact while E * nv < 2^32 (checked on the host); nv == 1 (a window one
+  // vector wide) would wrap the multiplier to 0, so it divides by 1 directly (uniform branch)
+  const uint32_t magic = nv > 1 ? 0xFFFFFFFFu / nv + 1u : 0u;
   uint32_t kmin = ~0u, kmax = 0u;
   for (int b = 0; b < st.channels; b++) {
     const T* base = (const T*)raster + st.base_off + (int64_t)b * st.band_stride + (int64_t)r0 * st.row_stride;
@@ -131,7 +132,7 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
 #pragma unroll
       for (int u = 0; u < U; u++) {  // items past E re-read item E-1 (idempotent for min/max)
         const uint32_t idx = min(i0 + (uint32_t)(u * 256) + threadIdx.x, E - 1);
-        const uint32_t r = __umulhi(idx, magic), v = idx - r * nv;
+        const uint32_t r = nv > 1 ? __umulhi(idx, magic) : idx, v = idx - r * nv;
         x[u] = *(const VT*)(base + (int64_t)r * st.row_stride + (int64_t)v * V);
       }
 #pragma unroll
@@ -162,9 +163,9 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
 }
 
 __global__ void k_frame_bytes(JobArgs a) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g > a.nframes_total) return;
-  if (g == a.nframes_total) { a.frame_bytes[g] = 0; return; }  // scan input tail
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.frame_count) return;
+  const int g = a.frame_base + i;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   uint8_t h[4 * kHdrWords];
@@ -265,7 +266,36 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
 }
 
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
-  k_frame_bytes<<<(a.nframes_total + 1 + 255) / 256, 256, 0, s>>>(a);
+  if (a.frame_count > 0) k_frame_bytes<<<(a.frame_count + 255) / 256, 256, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+// Frame group -> global byte offsets.  frame_off[f0, f0 + n) holds the group's own exclusive scan;
+// gbase[grp] (written by the previous group's launch, ordered by an event) is the byte offset of the
+// group's first frame.  Adds it, publishes gbase[grp + 1] and, for the last group, frame_off[nframes].
+__global__ void k_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
+                                unsigned long long* gbase, int grp, int f0, int n, int last, int nframes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long base = grp == 0 ? 0ull : gbase[grp];
+  if (i < n) {
+    const unsigned long long loc = frame_off[f0 + i];
+    frame_off[f0 + i] = loc + base;
+    if (i == n - 1) {
+      const unsigned long long end = base + loc + frame_bytes[f0 + i];
+      gbase[grp + 1] = end;
+      if (last) frame_off[nframes] = end;
+    }
+  } else if (i == 0) {  // empty group
+    gbase[grp + 1] = base;
+    if (last) frame_off[nframes] = base;
+  }
+}
+
+hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
+                                unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
+                                hipStream_t s) {
+  k_group_offsets<<<((n > 1 ? n : 1) + 255) / 256, 256, 0, s>>>(frame_off, frame_bytes, gbase, grp, f0, n, last,
+                                                              nframes);
   return hipGetLastError();
 }
 

@@ -76,7 +76,7 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int g = blockIdx.x;
+  const int g = a.frame_base + (int)blockIdx.x;
   {
     const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
     const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   const int64_t kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
 #ifdef FRA_GUARD
-  const uint64_t TOT = a.frame_off[a.nframes_total];
+  const uint64_t TOT = a.out_cap;  // frame_off[nframes_total] is final only after the last frame group
   const uint64_t SLOTW = (uint64_t)a.nframes_total * a.cmax * a.tmp_stride;
   {
     const FrameDev frg = a.frames[g];
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
 }
 
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s) {
-  if (a.nframes_total > 0) k_assemble<<<(unsigned)a.nframes_total, kThreads, 0, s>>>(a);
+  if (a.frame_count > 0) k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);
   return hipGetLastError();
 }
 

@@ -174,3 +174,29 @@ def test_synth_matches_numpy_mirror():
             ctx.free(dev)
         exp = synth_window(kind, 99, bands, H, W)
         assert np.array_equal(got, exp), kind
+
+
+@pytest.mark.parametrize("groups", [2, 3, 8])
+def test_frame_groups_pipelined_equal_serial(monkeypatch, groups):
+    """fra_plan_execute with FRA_GROUPS > 1 (window runs on their own streams, per-group scans joined by
+    k_group_offsets) must give the same stream table and bytes as the serial plan; a few streams are
+    also checked against the oracle.  >= 4096 frames so the plan really splits."""
+    H, W = 2048, 8200
+    r = synth_window(3, 21, 1, H, W)
+    wins = tiles(H, W, 512) + [(0, 0, 0, 0)]  # an empty window in the last group
+    monkeypatch.setenv("FRA_GROUPS", "1")
+    i1, f1 = N.encode_windows(r, wins, level=5, norm=16)
+    monkeypatch.setenv("FRA_GROUPS", str(groups))
+    ig, fg = N.encode_windows(r, wins, level=5, norm=16)
+    assert fg == f1
+    assert [(a.offset, a.frame_bytes, a.nframes) for a in ig] == [(a.offset, a.frame_bytes, a.nframes) for a in i1]
+    check_windows(r, [wins[0], wins[len(wins) // 2], wins[-2]], 5, 16)
+
+
+def test_minmax_one_vector_wide_windows():
+    """Windows exactly one load vector wide (8 int16 / 16 uint8 / 4 float32 columns) take the vectorised
+    min/max path with one vector per row (regression: its row divisor wrapped to 0)."""
+    for dt, w in ((np.int16, 8), (np.uint8, 16), (np.float32, 4)):
+        r = synth_window(3, 5, 2, 96, 64).astype(dt)
+        wins = [(0, 0, 96, 32), (0, 64 - w, 96, w), (32, 32, 64, w)]
+        check_windows(r, wins, 5, 16)
