@@ -231,15 +231,22 @@ __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kM
     T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
   }
-  g1 = -1;
-  g2 = -1;
+  // branch-free selects on uniform values (a branchy form let the compiler merge g1/g2 into a
+  // dynamically indexed private array, i.e. scratch memory)
+  int h1 = -1, h2 = -1;
   uint64_t b1 = 0, b2 = 0;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
-    if (!__builtin_amdgcn_readfirstlane(mvalid[k])) continue;
-    if (g1 < 0 || T[k] < b1) { b2 = b1; g2 = g1; b1 = T[k]; g1 = k; }
-    else if (g2 < 0 || T[k] < b2) { b2 = T[k]; g2 = k; }
+    const bool valid = __builtin_amdgcn_readfirstlane(mvalid[k]) != 0;
+    const bool lt1 = valid && (h1 < 0 || T[k] < b1);
+    const bool lt2 = valid && !lt1 && (h2 < 0 || T[k] < b2);
+    b2 = lt1 ? b1 : (lt2 ? T[k] : b2);
+    h2 = lt1 ? h1 : (lt2 ? k : h2);
+    b1 = lt1 ? T[k] : b1;
+    h1 = lt1 ? k : h1;
   }
+  g1 = __builtin_amdgcn_readfirstlane(h1);
+  g2 = __builtin_amdgcn_readfirstlane(h2);
 }
 
 // Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at

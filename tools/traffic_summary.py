@@ -37,13 +37,13 @@ write = per_kernel(src / "pmc_write", "WRITE_SIZE")
 lines = ["# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), python bench.py --steps 3 "
          "--warmup 1 --no-cpu --no-e2e (C4, level 5, 1 GPU)",
          "# FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports 1/2 of wide coalesced reads); counters in KiB -> bytes",
-         "# kernel, launches, FETCH raw MB/launch, FETCH x2 MB, WRITE MB, traffic MB per launch (fetch x2 + write)"]
+         "# kernel, launches, median over launches: FETCH raw MB/launch, FETCH x2 MB, WRITE MB, traffic MB per launch (fetch x2 + write)"]
 traffic = {}
 for k in sorted(set(fetch) | set(write), key=short):
     f = fetch.get(k, [0.0])
     w = write.get(k, [0.0])
-    fr = sum(f) / len(f)
-    wr = sum(w) / len(w)
+    fr = sorted(f)[len(f) // 2]  # median launch: the small in-run parity launches are not C4 launches
+    wr = sorted(w)[len(w) // 2]
     t = 2 * fr + wr
     lines.append(f"{short(k):40s} {len(f):4d} {fr / 1e6:10.2f} {2 * fr / 1e6:10.2f} {wr / 1e6:10.2f} {t / 1e6:10.2f}")
     nm = short(k)
