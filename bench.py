@@ -116,7 +116,8 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist_mod
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # RCCL over xGMI on a GPU node; FRA_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        backend = os.environ.get("FRA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist_mod.init_process_group(backend=backend)

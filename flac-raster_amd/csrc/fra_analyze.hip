@@ -949,7 +949,7 @@ read_x28(S.smp, t, x);
         for (int jj = 0; jj < kChunk; jj++) {
           if (live && !(jj < 12 && head && jj < o)) {
             const uint32_t qv = uu[jj] >> kcur;
-            lds_put(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
+            lds_put2(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
             p += qv + 1u + (uint32_t)kcur;
           }
         }
@@ -1192,7 +1192,7 @@ read_x28(S.smp, t, x);
       for (int jj = 0; jj < kChunk; jj++) {
         if (live && !(jj < 12 && head && jj < o)) {
           const uint32_t qv = uu[jj] >> kcur;
-          lds_put(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
+          lds_put2(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
           p += qv + 1u + (uint32_t)kcur;
         }
       }
@@ -1223,7 +1223,7 @@ read_x28(S.smp, t, x);
         const int k = (int)(kk[jj] & 0xFF);
         if (kk[jj] & 0x100u) { lds_put(buf, p, (uint32_t)k, pb); p += pb; }
         const uint32_t qv = uu[jj] >> k;
-        lds_put(buf, p + qv, (k == 0) ? 1u : ((1u << k) | (uu[jj] & ((1u << k) - 1u))), k + 1);
+        lds_put2(buf, p + qv, (k == 0) ? 1u : ((1u << k) | (uu[jj] & ((1u << k) - 1u))), k + 1);
         p += qv + 1u + (uint32_t)k;
       }
     }

@@ -704,6 +704,16 @@ __device__ __forceinline__ void lds_put(uint32_t* buf, uint32_t pos, uint32_t v,
   }
 }
 
+// Branch-free variant for the residual loops: always ORs into words w0 and w0 + 1 (the second OR may
+// be of zero bits), so a wave issues two LDS ops per code instead of three when its lanes split
+// over the two cases.  Needs one spare zeroed word after the last one written.
+__device__ __forceinline__ void lds_put2(uint32_t* buf, uint32_t pos, uint32_t v, int width) {
+  const uint32_t w0 = pos >> 5;
+  const uint64_t x = ((uint64_t)v << (64 - width)) >> (pos & 31);
+  atomicOr(&buf[w0], (uint32_t)(x >> 32));
+  atomicOr(&buf[w0 + 1], (uint32_t)x);
+}
+
 // ---------------------------------------------------------------- frame header (RFC 9639 9.1)
 __host__ __device__ inline int utf8_len(uint32_t v) {
   if (v < 0x80) return 1;
