@@ -158,18 +158,17 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   uint32_t acc = 0;
   int64_t q0 = (int64_t)t - pad;  // quad index in v/4 space
   if (q0 < 0) q0 += kThreads;
-  for (; q0 < NQW; q0 += (int64_t)kThreads * U) {
-    uint32_t w[U][5], sh[U];
-    bool fast[U];
+  // slot gather of the U quads of round q0 (fast case: one 16-byte + one dword load, shift later)
+  auto fetch = [&](const int64_t qr, uint32_t (&w)[U][5], uint32_t (&sh)[U], bool (&fast)[U]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t k = 4 * (q0 + (int64_t)u * kThreads) - a4;  // first dword of the quad
+      const int64_t k = 4 * (qr + (int64_t)u * kThreads) - a4;  // first dword of the quad
       const int64_t bp = 8 * (4 * k - (int64_t)A);
       fast[u] = false;
       sh[u] = 0;
 #pragma unroll
       for (int i = 0; i < 5; i++) w[u][i] = 0;
-      if (k >= 0 && k + 4 <= ND && bp >= (int64_t)sg[1] && bp + 128 <= (int64_t)TB) {
+      if (qr + (int64_t)u * kThreads < NQW && k >= 0 && k + 4 <= ND && bp >= (int64_t)sg[1] && bp + 128 <= (int64_t)TB) {
         const uint32_t b = (uint32_t)bp;
         int sgi = 1;  // blob sgi - 1 holds bit b: sg[sgi] <= b < sg[sgi + 1]
 #pragma unroll
@@ -190,6 +189,22 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
         }
       }
     }
+  };
+  uint32_t wn[U][5], shn[U];
+  bool fastn[U];
+  if (q0 < NQW) fetch(q0, wn, shn, fastn);
+  for (; q0 < NQW; q0 += (int64_t)kThreads * U) {
+    uint32_t w[U][5], sh[U];
+    bool fast[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      fast[u] = fastn[u];
+      sh[u] = shn[u];
+#pragma unroll
+      for (int i = 0; i < 5; i++) w[u][i] = wn[u][i];
+    }
+    // next round's loads are in flight while this round is shifted, stored and CRC'd
+    if (q0 + (int64_t)kThreads * U < NQW) fetch(q0 + (int64_t)kThreads * U, wn, shn, fastn);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t q = q0 + (int64_t)u * kThreads;
