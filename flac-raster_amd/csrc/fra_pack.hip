@@ -77,18 +77,6 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = a.frame_base + (int)blockIdx.x;
-  {
-    const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
-    const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
-    uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
-    uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
-    constexpr int NT = 16 * 256 * 2 / 16, NM = kMLevels * 512 * 2 / 16;
-    for (int i = t; i < NT + NM; i += kThreads) {
-      if (i < NT) dT[i] = srcT[i];
-      else dM[i - NT] = srcM[i - NT];
-    }
-    if (t < kMetaWords) S.meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
-  }
   const uint16_t* M = &S.M[0][0];
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
@@ -101,7 +89,6 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
 #pragma unroll
   for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = __builtin_amdgcn_readfirstlane(gmeta[kHdrWords + i]);
-  __syncthreads();
   const uint32_t* hdrw = S.meta;
   const uint32_t* seg = S.meta + kHdrWords;
   const uint32_t TB = sg[C + 1];                // frame bits before the byte pad
@@ -193,6 +180,20 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   uint32_t wn[U][5], shn[U];
   bool fastn[U];
   if (q0 < NQW) fetch(q0, wn, shn, fastn);
+  // CRC tables and header words to LDS while the first slot loads are in flight
+  {
+    const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
+    const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
+    uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
+    uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
+    constexpr int NT = 16 * 256 * 2 / 16, NM = kMLevels * 512 * 2 / 16;
+    for (int i = t; i < NT + NM; i += kThreads) {
+      if (i < NT) dT[i] = srcT[i];
+      else dM[i - NT] = srcM[i - NT];
+    }
+    if (t < kMetaWords) S.meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
+  }
+  __syncthreads();
   for (; q0 < NQW; q0 += (int64_t)kThreads * U) {
     uint32_t w[U][5], sh[U];
     bool fast[U];
