@@ -447,6 +447,7 @@ read_x28(S.smp, t, x);
       if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], 2ull * s32);
     }
   }
+  FRA_STOP(9)
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = !B32 && fastframe && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
@@ -524,6 +525,7 @@ read_x28(S.smp, t, x);
         window_acf(wi, wl, act);
       }
       __syncthreads();
+      FRA_STOP(8)
       if constexpr (MAXLAG <= 8) {
         // levels 3-6 (<= 3 windows): the two FIXED candidates on waves 1-2 while wave 0 runs the
         // Levinson-Durbin of EVERY window at once, window w on lanes 16w..16w+15 (the same op sequence
