@@ -946,13 +946,15 @@ read_x28(S.smp, t, x);
         uint32_t p = pos + inc - tot;
         for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
         if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
-        const uint32_t kmask = (1u << kcur) - 1u;
+        // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
+        const uint32_t sal = 31u - (uint32_t)kcur;
+        const uint32_t mal = ((1u << kcur) - 1u) << sal;
 #pragma unroll
         for (int jj = 0; jj < kChunk; jj++) {
           if (live && !(jj < 12 && head && jj < o)) {
-            const uint32_t qv = uu[jj] >> kcur;
-            lds_put2(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
-            p += qv + 1u + (uint32_t)kcur;
+            const uint32_t P = p + (uu[jj] >> kcur);
+            lds_put_al(buf, P, ((uu[jj] << sal) & mal) | 0x80000000u);
+            p = P + 1u + (uint32_t)kcur;
           }
         }
       }
@@ -1189,13 +1191,15 @@ read_x28(S.smp, t, x);
       uint32_t p = pos + inc - tot;
       for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
       if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
-      const uint32_t kmask = (1u << kcur) - 1u;
+      // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
+      const uint32_t sal = 31u - (uint32_t)kcur;
+      const uint32_t mal = ((1u << kcur) - 1u) << sal;
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
         if (live && !(jj < 12 && head && jj < o)) {
-          const uint32_t qv = uu[jj] >> kcur;
-          lds_put2(buf, p + qv, (1u << kcur) | (uu[jj] & kmask), kcur + 1);
-          p += qv + 1u + (uint32_t)kcur;
+          const uint32_t P = p + (uu[jj] >> kcur);
+          lds_put_al(buf, P, ((uu[jj] << sal) & mal) | 0x80000000u);
+          p = P + 1u + (uint32_t)kcur;
         }
       }
     } else {

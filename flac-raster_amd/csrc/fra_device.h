@@ -714,6 +714,14 @@ __device__ __forceinline__ void lds_put2(uint32_t* buf, uint32_t pos, uint32_t v
   atomicOr(&buf[w0 + 1], (uint32_t)x);
 }
 
+// A code left-aligned in 32 bits (its first bit at bit 31, zeros below its last bit) written at bit
+// position P: both words it can touch are ORed unconditionally (shift counts use P mod 32 in hardware).
+__device__ __forceinline__ void lds_put_al(uint32_t* buf, uint32_t P, uint32_t cal) {
+  const uint32_t w0 = P >> 5;
+  atomicOr(&buf[w0], cal >> (P & 31u));
+  atomicOr(&buf[w0 + 1], __builtin_amdgcn_alignbit(cal, 0u, P & 31u));
+}
+
 // ---------------------------------------------------------------- frame header (RFC 9639 9.1)
 __host__ __device__ inline int utf8_len(uint32_t v) {
   if (v < 0x80) return 1;
