@@ -110,6 +110,9 @@ struct AnalyzeSmem {
   int32_t mcoef[kMaxModels][kMaxLpc];
   int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
+  // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
+  // partition order (written by porder_search, read by the winner's exact pass)
+  uint8_t kbest[B32 ? 1 : kMaxModels][kMaxPart];
   uint32_t ired[4][3];
   uint32_t scan[4];
   int32_t winner, ftype, fmethod;
@@ -255,7 +258,8 @@ __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kM
 // lane group [2^p, 2^(p+1)), summed after p steps) and one ballot.  Same totals and tie rule as the
 // oracle's per-level loop (iterate p = pm..0, keep '<=').
 __device__ __forceinline__ void porder_search(const unsigned long long* psum, unsigned long long* node, int P, int pm,
-                                              int n, int o, int lane, uint64_t& best_out, int& bp_out) {
+                                              int n, int o, int lane, uint64_t& best_out, int& bp_out,
+                                              uint8_t* kout = nullptr) {
   // node sums: finest sums S_j, then upper-lane group sums (leader lane of 2^s lanes = (j+1)2^s - 1)
   uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
   if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
@@ -280,14 +284,14 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
   uint32_t bits32 = 0;
   bool big = false;
   const int p = lane ? 31 - __clz(lane) : 0;
+  int kn = 0;
   if (lane >= 1 && p <= P && p <= pm) {
     const int j = lane - (1 << p);
     const uint64_t cnt = (uint64_t)((n >> p) - (j == 0 ? o : 0));
-    int k;
     uint64_t bits;
-    rice_pick(cnt, node[lane], k, bits);
+    rice_pick(cnt, node[lane], kn, bits);
     bits32 = (uint32_t)bits;
-    big = k > 14;
+    big = kn > 14;
   }
   const uint64_t bigm = __ballot(big);
   uint32_t tot[7];
@@ -305,13 +309,13 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
   tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
   tot[6] = 0;
   bool big6 = false;
+  int k6 = 0;
   if (P == 6 && pm == 6) {  // level 6: 64 nodes at node[64 + lane]
     const uint64_t cnt = (uint64_t)((n >> 6) - (lane == 0 ? o : 0));
-    int k;
     uint64_t bits;
-    rice_pick(cnt, node[64 + lane], k, bits);
+    rice_pick(cnt, node[64 + lane], k6, bits);
     tot[6] = wave_sum32((uint32_t)bits);
-    big6 = __any(k > 14);
+    big6 = __any(k6 > 14);
   }
   uint64_t best = 0;
   int bp = pm;
@@ -322,6 +326,10 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
   }
   best_out = best;
   bp_out = bp;
+  if (kout) {  // the chosen order's per-partition estimates (node (bp, j) at lane 2^bp + j)
+    if (bp == 6) kout[lane] = (uint8_t)k6;
+    else if (lane >= (1 << bp) && lane < (2 << bp)) kout[lane - (1 << bp)] = (uint8_t)kn;
+  }
 }
 
 template <bool B32, int MAXLAG>
@@ -540,7 +548,7 @@ read_x28(S.smp, t, x);
             const int pm = max_porder(n, m, cfg.max_porder);
             uint64_t best = 0;
             int bp = pm;
-            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp);
+            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
             if (lane == 0) {
               S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
               S.mporder[m] = bp;
@@ -610,7 +618,7 @@ read_x28(S.smp, t, x);
             const int pm = max_porder(n, m, cfg.max_porder);
             uint64_t best = 0;
             int bp = pm;
-            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp);
+            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
             if (lane == 0) {
               S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
               S.mporder[m] = bp;
@@ -762,7 +770,7 @@ read_x28(S.smp, t, x);
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp);
+    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
@@ -788,26 +796,11 @@ read_x28(S.smp, t, x);
       const int o = __builtin_amdgcn_readfirstlane(S.morder[m]);
       const int sh = __builtin_amdgcn_readfirstlane(S.mshift[m]);
       const int ps = __builtin_amdgcn_readfirstlane(S.mporder[m]);
-      // estimate k per partition of order ps: upper-lane sums of the finest sums (3.8), leader lane
-      // ((j+1) << smax) - 1 of partition j holds its k
-      const int smax = P - ps;
-      uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
-      if (smax > 0) Sv = up_add64<0>(Sv);
-      if (smax > 1) Sv = up_add64<1>(Sv);
-      if (smax > 2) Sv = up_add64<2>(Sv);
-      if (smax > 3) Sv = up_add64<3>(Sv);
-      if (smax > 4) Sv = up_add64<4>(Sv);
-      if (smax > 5) Sv = up_add64<5>(Sv);
-      int kl;
-      {
-        const int j = lane >> smax;
-        uint64_t bits;
-        rice_pick((uint64_t)((n >> ps) - (j == 0 ? o : 0)), Sv, kl, bits);
-      }
+      // estimate k per partition of order ps (3.8): stored by the winner's porder_search
       const int pz = n >> ps;
       const bool live = i0 < n;
       const int pidx = live ? i0 / pz : 0;
-      const int k0 = __shfl(kl, ((pidx + 1) << smax) - 1, 64);
+      const int k0 = S.kbest[B32 ? 0 : m][pidx];
       // zig-zag residuals of the winner (exact code values), warm-up samples 0
       uint32_t uu[kChunk];
 read_x28(S.smp, t, x);
@@ -853,10 +846,20 @@ read_x28(S.smp, t, x);
         // is entirely live or entirely past n.
         const int ls = min(6, 31 - __builtin_clz((uint32_t)tpp));
         uint64_t v0 = fs0, v1 = fs1, v2 = fs2;
-#define FRA_UP(S_)                                                                     \
-        if (ls > S_) { v0 = up_add64<S_>(v0); v1 = up_add64<S_>(v1); v2 = up_add64<S_>(v2); }
-        FRA_UP(0) FRA_UP(1) FRA_UP(2) FRA_UP(3) FRA_UP(4) FRA_UP(5)
+        if (__all(fs0 <= (0xFFFFFFFFu >> ls))) {
+          // 2^ls lanes of at most 2^(32-ls) - 1 (fs0 >= fs1 >= fs2): the group sums fit 32 bits
+          uint32_t u0 = fs0, u1 = fs1, u2 = fs2;
+#define FRA_UP(S_) \
+          if (ls > S_) { u0 = up_add32<S_>(u0); u1 = up_add32<S_>(u1); u2 = up_add32<S_>(u2); }
+          FRA_UP(0) FRA_UP(1) FRA_UP(2) FRA_UP(3) FRA_UP(4) FRA_UP(5)
 #undef FRA_UP
+          v0 = u0; v1 = u1; v2 = u2;
+        } else {
+#define FRA_UP(S_)                                                                     \
+          if (ls > S_) { v0 = up_add64<S_>(v0); v1 = up_add64<S_>(v1); v2 = up_add64<S_>(v2); }
+          FRA_UP(0) FRA_UP(1) FRA_UP(2) FRA_UP(3) FRA_UP(4) FRA_UP(5)
+#undef FRA_UP
+        }
         const int gm = (1 << ls) - 1;
         if (live && (lane & gm) == gm) {
           atomicAdd(&S.nu.e.esum2[pidx][0], (unsigned long long)v0);
@@ -872,7 +875,7 @@ read_x28(S.smp, t, x);
       FRA_STOP(6)
       // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
       const int npp = 1 << ps;
-      const int k0j = __shfl(kl, lane < npp ? ((lane + 1) << smax) - 1 : 0, 64);
+      const int k0j = lane < npp ? (int)S.kbest[B32 ? 0 : m][lane] : 0;
       uint64_t best = 0;
       int bk = 0;
       if (lane < npp) {

@@ -270,6 +270,15 @@ __device__ __forceinline__ uint64_t up_add64(uint64_t v) {
   else if constexpr (S == 4) return v + dpp64<DPP_BC15, 0xA>(v);
   else return v + dpp64<DPP_BC31, 0xC>(v);
 }
+template <int S>
+__device__ __forceinline__ uint32_t up_add32(uint32_t v) {
+  if constexpr (S == 0) return v + dpp32<DPP_SHR1, 0xF>(v);
+  else if constexpr (S == 1) return v + dpp32<DPP_SHR2, 0xF>(v);
+  else if constexpr (S == 2) return v + dpp32<DPP_SHR4, 0xF>(v);
+  else if constexpr (S == 3) return v + dpp32<DPP_SHR8, 0xF>(v);
+  else if constexpr (S == 4) return v + dpp32<DPP_BC15, 0xA>(v);
+  else return v + dpp32<DPP_BC31, 0xC>(v);
+}
 // FRA-1 autocorrelation tree over one wave's 64 chunk partials; result at lane 63
 __device__ __forceinline__ double tree64(double v) {
   v = v + dppf64<DPP_SHR1, 0xF>(v);
