@@ -104,6 +104,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.level is not None:
