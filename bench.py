@@ -7,25 +7,35 @@ Workload (default ``--config c4``, the north-star configuration of BASELINE.json
 A *step* = one pass of the encode hot path over the whole scene: device-resident raster in HBM ->
 per-tile nanmin/nanmax -> normalize_to_audio -> FLAC analysis -> bit-packed frames of every tile
 in HBM (the bytes the reference's pyflac/libFLAC calls produce per tile, cli.py:553-622).
-Multi-GPU (one process per GPU, torch.distributed.run): weak scaling by default -- every rank
-encodes its own C4 scene (seed 20260227 + rank, generated in its HBM), i.e. the job is N scenes
-sharded one per GPU with no collective on the data path; ``value`` = pixels of all ranks' scenes /
-max-over-ranks time.  ``--scaling strong`` instead splits ONE scene's tiles over the ranks (LPT on
-pixel count).
 
-Also reported: ``roofline`` of the dominant kernel (HIP events on the plan's stream, algorithmic
-bytes = input raster bytes + emitted frame bytes of the units one launch processes), and
-``cpu_baseline`` = the CPU oracle (oracle/, C port, 1 core) timed on a bounded sample of the same
-scene, whose bytes are also checked against the GPU's (in-run parity).
+Multi-GPU (one process per GPU, torch.distributed.run): STRONG scaling by default -- BASELINE's C4/C5
+are ONE scene whose tiles are sharded over the GPUs (LPT on pixel count), no collective
+on the data path; ``value`` = scene pixels / max-over-ranks time; per-rank times and the imbalance are
+reported.  ``--scaling weak`` instead gives every rank its own scene (seed + rank).
+
+Also reported (rank 0):
+* ``roofline`` of the dominant kernel: HIP events on the plan's stream; algorithmic bytes = input raster
+  bytes + emitted frame bytes of the units one launch processes; ``traffic`` / ``valu_issue_frac`` from
+  in-run rocprofv3 PMC passes of this same build (``--no-pmc`` falls back to the committed profile
+  file of the same kernel sources, else null); ``bound`` = the larger of the HBM and VALU-issue fractions;
+* ``cpu_baseline``: the CPU oracle (oracle/, C port of the path, 1 thread) on a bounded sample of the
+  same scene, bytes checked against the GPU's; ``cpu_baseline_mp``: the same port fanned over the
+  host's core share (BASELINE.md B-mp);
+* ``e2e``: the PCIe-inclusive path (host raster -> pipelined H2D / kernels / D2H -> host frames).
 """
 
 from __future__ import annotations
 
 import argparse
+import csv
+import hashlib
 import json
 import os
 import platform
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -44,7 +54,10 @@ CONFIGS = {
                         "--tile-size 512, -c 8"),
 }
 SEED = 20260227
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level parameters)
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level parameters)
+SIMDS = 256 * 4          # 256 CUs x 4 SIMD-32
+VALU_CYC = 2             # SIMD cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
+XCDS = 8                 # GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs
 
 
 def tiles(H, W, t):
@@ -52,7 +65,7 @@ def tiles(H, W, t):
 
 
 def lpt_shard(wins, nranks):
-    """Longest-processing-time static assignment of tiles to ranks (deterministic)."""
+    """Longest-processing-time static assignment of tiles to ranks (deterministic; == dist.shard)."""
     order = sorted(range(len(wins)), key=lambda i: (-(wins[i][2] * wins[i][3]), i))
     load = [0] * nranks
     owner = [0] * len(wins)
@@ -63,11 +76,35 @@ def lpt_shard(wins, nranks):
     return owner
 
 
-def cpu_baseline(cfg, wins, gpu_frames, gpu_infos, budget_s):
+def sources_sha():
+    """Hash of the kernel sources: a committed profile file is only valid for the build it measured."""
+    h = hashlib.sha256()
+    for p in sorted((ROOT / "flac-raster_amd" / "csrc").glob("*")):
+        if p.suffix in (".hip", ".h", ".cpp"):
+            h.update(p.name.encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+# ------------------------------------------------------------------------------------- CPU baselines
+def _oracle():
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # test / baseline infrastructure only (never on the product path)
+    return O
+
+
+def _encode_tile_cpu(O, cfg, tile):
+    B = cfg["bands"]
+    h, w = tile.shape[1], tile.shape[2]
+    inter = tile.transpose(1, 2, 0).reshape(-1, B)
+    audio, _, _ = O.normalize(inter, 16 if cfg["norm"] == 16 else 24)
+    return O.encode(audio, O.sample_rate_for_pixels(h * w), level=cfg["level"], with_header=False)
+
+
+def cpu_baseline(cfg, wins, gpu_tile_bytes, budget_s):
     """Time the CPU oracle (C port of the encode path, 1 thread) on the first tiles of the scene
     until ~budget_s of CPU work; verify its bytes equal the GPU's for those tiles."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle as O  # test/baseline infrastructure only
+    O = _oracle()
     from flac_raster.synth import synth_window
 
     px = 0
@@ -77,15 +114,13 @@ def cpu_baseline(cfg, wins, gpu_frames, gpu_infos, budget_s):
     for idx, (r0, c0, h, w) in enumerate(wins):
         tile = synth_window(cfg["kind"], SEED, cfg["bands"], cfg["H"], cfg["W"], r0, c0, h, w)
         t0 = time.perf_counter()
-        inter = tile.transpose(1, 2, 0).reshape(-1, cfg["bands"])
-        audio, _, _ = O.normalize(inter, 16 if cfg["norm"] == 16 else 24)
-        frames = O.encode(audio, O.sample_rate_for_pixels(h * w), level=cfg["level"], with_header=False)
+        frames = _encode_tile_cpu(O, cfg, tile)
         t_cpu += time.perf_counter() - t0
         px += h * w
-        if idx in gpu_infos:
-            info = gpu_infos[idx]
+        got = gpu_tile_bytes(idx)
+        if got is not None:
             checked += 1
-            if gpu_frames[info.offset: info.offset + info.frame_bytes] != frames:
+            if got != frames:
                 mismatches += 1
         if t_cpu >= budget_s:
             break
@@ -93,6 +128,135 @@ def cpu_baseline(cfg, wins, gpu_frames, gpu_infos, budget_s):
                 mismatches=mismatches)
 
 
+def _mp_worker(args):
+    cfg_name, level, tile_ids, barrier = args
+    cfg = dict(CONFIGS[cfg_name], level=level)
+    O = _oracle()
+    from flac_raster.synth import synth_window
+
+    wins = tiles(cfg["H"], cfg["W"], cfg["tile"])
+    data = [synth_window(cfg["kind"], SEED, cfg["bands"], cfg["H"], cfg["W"], *wins[i]) for i in tile_ids]
+    barrier.wait()
+    t0 = time.perf_counter()
+    nbytes = 0
+    for t in data:
+        nbytes += len(_encode_tile_cpu(O, cfg, t))
+    t1 = time.perf_counter()
+    return t0, t1, sum(wins[i][2] * wins[i][3] for i in tile_ids), nbytes
+
+
+def cpu_mp_child(cfg_name, procs, ntiles, level=None):
+    """B-mp: the oracle on the first ``ntiles`` tiles fanned over ``procs`` processes (its own process
+    tree, started by the bench as a child so no GPU state is forked); prints one JSON line."""
+    import multiprocessing as mp
+
+    cfg = CONFIGS[cfg_name]
+    level = cfg["level"] if level is None else level
+    wins = tiles(cfg["H"], cfg["W"], cfg["tile"])[:ntiles]
+    order = sorted(range(len(wins)), key=lambda i: -(wins[i][2] * wins[i][3]))
+    share = [[] for _ in range(procs)]
+    load = [0] * procs
+    for i in order:
+        k = min(range(procs), key=lambda j: load[j])
+        share[k].append(i)
+        load[k] += wins[i][2] * wins[i][3]
+    share = [s for s in share if s]
+    ctx = mp.get_context("fork")
+    mgr = ctx.Manager()
+    barrier = mgr.Barrier(len(share))
+    with ctx.Pool(len(share)) as pool:
+        res = pool.map(_mp_worker, [(cfg_name, level, s, barrier) for s in share])
+    t0 = min(r[0] for r in res)
+    t1 = max(r[1] for r in res)
+    px = sum(r[2] for r in res)
+    print(json.dumps({"value": px / (t1 - t0) / 1e6, "seconds": t1 - t0, "pixels": px, "tiles": len(wins),
+                      "procs": len(share)}), flush=True)
+
+
+# ------------------------------------------------------------------------------------- in-run PMC
+def _short(name):
+    return name.replace("void ", "").split("(")[0].replace("fra::", "").split("<")[0]
+
+
+def pmc_pass(args, counters, tag):
+    """One rocprofv3 counter pass over a 1-step child run of this bench (same config, same build).
+    Returns {kernel: {counter: [values per launch]}} or None."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    out = tempfile.mkdtemp(prefix=f"fra_pmc_{tag}_", dir="/tmp")
+    cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
+           sys.executable, str(ROOT / "bench.py"), "--config", args.config, "--steps", "1", "--warmup", "1",
+           "--child"]
+    if args.level is not None:
+        cmd += ["--level", str(args.level)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=float(os.environ.get("FRA_PMC_TIMEOUT", "150")), check=True)
+    except (subprocess.SubprocessError, OSError):
+        shutil.rmtree(out, ignore_errors=True)
+        return None
+    f = next(Path(out).rglob("*counter_collection.csv"), None)
+    acc = {}
+    if f is not None:
+        for r in csv.DictReader(open(f)):
+            acc.setdefault(_short(r["Kernel_Name"]), {}).setdefault(r["Counter_Name"], []).append(
+                float(r["Counter_Value"]))
+    shutil.rmtree(out, ignore_errors=True)
+    return acc or None
+
+
+def _med(v):
+    v = sorted(v or [0.0])
+    return v[len(v) // 2]
+
+
+def inrun_pmc(args, kernel):
+    """HBM traffic (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction; KiB) and VALU
+    instruction counts of ``kernel``'s median launch, from separate passes."""
+    res = {"source": "in-run rocprofv3 --pmc passes of this build (bench.py --child, 1 step)"}
+    fe = pmc_pass(args, ["FETCH_SIZE"], "fetch")
+    wr = pmc_pass(args, ["WRITE_SIZE"], "write")
+    va = pmc_pass(args, ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"], "valu")
+    gr = pmc_pass(args, ["GRBM_GUI_ACTIVE"], "grbm")
+    if fe and wr and kernel in fe and kernel in wr:
+        res["traffic"] = int(2 * _med(fe[kernel]["FETCH_SIZE"]) * 1024 + _med(wr[kernel]["WRITE_SIZE"]) * 1024)
+        res["traffic_by_kernel"] = {k: int(2 * _med(fe[k].get("FETCH_SIZE")) * 1024 +
+                                           _med(wr.get(k, {}).get("WRITE_SIZE")) * 1024) for k in fe}
+    if va and kernel in va:
+        v = va[kernel]
+        waves = _med(v.get("SQ_WAVES"))
+        res["waves"] = int(waves)
+        res["valu_insts"] = int(_med(v.get("SQ_INSTS_VALU")))
+        res["valu_per_wave"] = round(res["valu_insts"] / waves, 1) if waves else None
+        res["salu_per_wave"] = round(_med(v.get("SQ_INSTS_SALU")) / waves, 1) if waves else None
+        res["lds_per_wave"] = round(_med(v.get("SQ_INSTS_LDS")) / waves, 1) if waves else None
+    if gr and kernel in gr:
+        res["busy_cycles_per_xcd"] = int(_med(gr[kernel].get("GRBM_GUI_ACTIVE")) / XCDS)
+    return res
+
+
+def committed_profile(args, cfg, kernel):
+    f = ROOT / "profiles" / f"traffic_{args.config}.json"
+    if not f.exists():
+        return {"source": "none"}
+    try:
+        d = json.loads(f.read_text())
+    except ValueError:
+        return {"source": "unreadable"}
+    if d.get("sources_sha") != sources_sha():
+        return {"source": f"{d.get('source')} is STALE (kernel sources changed since it was measured)"}
+    out = {"source": d.get("source"), "traffic": d.get(kernel)}
+    for k in ("waves", "valu_insts", "valu_per_wave", "busy_cycles_per_xcd"):
+        if f"{kernel}:{k}" in d:
+            out[k] = d[f"{kernel}:{k}"]
+    return out
+
+
+# ------------------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,12 +264,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--level", type=int, default=None)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (rank 0)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of 1-core CPU oracle work (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)  # PMC child: steps only
+    ap.add_argument("--cpu-mp-child", nargs=2, type=int, metavar=("PROCS", "TILES"), help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_mp_child:
+        cpu_mp_child(args.config, *args.cpu_mp_child, level=args.level)
+        return
     cfg = dict(CONFIGS[args.config])
     if args.level is not None:
         cfg["level"] = args.level
@@ -130,23 +299,15 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def allmax(x: float) -> float:
+    def allgather(vals):
         if dist is None:
-            return x
+            return [list(vals)]
         import torch
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def allsum(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+        t = torch.tensor(list(vals), dtype=torch.float64, device=dev)
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [o.cpu().tolist() for o in out]
 
     ctx = N.Context(local if N.device_count() > local else 0)
     B, H, W = cfg["bands"], cfg["H"], cfg["W"]
@@ -161,6 +322,14 @@ def main():
     my_wins = [wins[i] for i in mine]
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
 
+    if args.child:  # rocprofv3 child: the plan's launches only
+        for _ in range(args.warmup + args.steps):
+            plan.execute()
+        plan.sync()
+        plan.close()
+        ctx.free(dev_raster)
+        return
+
     for _ in range(args.warmup):
         plan.execute()
     plan.sync()
@@ -168,12 +337,11 @@ def main():
     plan.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.execute()  # frame groups pipelined over streams
+        plan.execute()
     plan.sync()
     t1 = time.perf_counter()
     barrier()
     dt_s = t1 - t0
-    T = allmax(dt_s)
     # per-kernel launch times (roofline): the same steps again, serial, HIP events between kernels
     plan.enable_timing(True)
     for _ in range(args.steps):
@@ -184,62 +352,64 @@ def main():
     infos, total = plan.result()
     my_px = sum(w[2] * w[3] for w in my_wins)
     my_in_bytes = my_px * B * dt.itemsize
-    out_bytes_all = allsum(float(total))
+    per_launch_ms = [k / max(1, nexec) for k in kms]
+    ranks = allgather([dt_s, per_launch_ms[1], sum(per_launch_ms), len(my_wins), my_px, total])
+    T = max(r[0] for r in ranks)
+    out_bytes_all = sum(r[5] for r in ranks)
 
     # dominant kernel: the larger of analyze (1) and pack (3); algorithmic bytes per launch =
     # input bytes + frame bytes of the units this rank's launch processes
-    per_launch_ms = [k / max(1, nexec) for k in kms]
     dom = 1 if per_launch_ms[1] >= per_launch_ms[3] else 3
-    dom_name = {1: "k_analyze", 3: "k_pack"}[dom]
+    dom_name = {1: "k_analyze", 3: "k_assemble"}[dom]
     alg_bytes = my_in_bytes + total
     achieved = alg_bytes / (per_launch_ms[dom] * 1e-3) / 1e9
     step_ms_local = sum(per_launch_ms)
     path_gbps = alg_bytes / (step_ms_local * 1e-3) / 1e9
-
-    traffic = None
-    tfile = ROOT / "profiles" / f"traffic_{args.config}_l{cfg['level']}_n{world}.json"
-    if tfile.exists():
-        try:
-            traffic = json.loads(tfile.read_text()).get(dom_name)
-        except Exception:
-            traffic = None
 
     result = None
     if rank == 0:
         scene_px = H * W
         job_px = scene_px * (world if weak else 1)
         value = job_px * args.steps / T / 1e6
-        cpu = None
-        if not args.no_cpu and world >= 1:
-            _, frames = plan.download()
+        cpu = cpu_mp = None
+        if not args.no_cpu and world == 1:
             gi = {i: infos[j] for j, i in enumerate(mine)}
-            cb = cpu_baseline(cfg, wins, frames, gi, args.cpu_budget)
+            dev_out, _ = plan.device_output()
+
+            def tile_bytes(idx):  # this tile's frames, copied D2H on demand
+                if idx not in gi:
+                    return None
+                buf = np.empty(max(1, gi[idx].frame_bytes), np.uint8)
+                N.load().fra_memcpy_d2h(ctx.h, buf.ctypes.data, dev_out + gi[idx].offset, gi[idx].frame_bytes)
+                return buf[:gi[idx].frame_bytes].tobytes()
+            cb = cpu_baseline(cfg, wins, tile_bytes, args.cpu_budget)
             cpu = {"value": round(cb["value"], 3), "unit": "MPix/s", "cores": 1, "kind": "port",
                    "sample": f"first {cb['tiles']} tiles ({cb['pixels']} px, {cb['seconds']:.1f} s) of the same "
                              f"scene through oracle/fr_oracle.c normalize+encode (FRA-1, 1 thread, "
                              f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}); "
                              f"bytes equal to GPU for {cb['checked'] - cb['mismatches']}/{cb['checked']} tiles"}
-        # PCIe-inclusive end-to-end (not `value`): host numpy raster -> H2D -> encode -> D2H frames
+            # B-mp: the same port over the host's core share (OMP_NUM_THREADS on the box = its CPU share)
+            procs = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+            px_per_tile = cb["pixels"] / max(1, cb["tiles"])
+            ntiles = int(min(len(wins), max(procs, cb["value"] * 1e6 * 6.0 * procs / max(1.0, px_per_tile))))
+            try:
+                r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", args.config,
+                                    "--cpu-mp-child", str(procs), str(ntiles)] +
+                                   (["--level", str(args.level)] if args.level is not None else []),
+                                   capture_output=True, text=True, timeout=240, check=True)
+                mp = json.loads(r.stdout.strip().splitlines()[-1])
+                cpu_mp = {"value": round(mp["value"], 3), "unit": "MPix/s", "cores": mp["procs"], "kind": "port",
+                          "sample": f"first {mp['tiles']} tiles ({mp['pixels']} px) over {mp['procs']} processes, "
+                                    f"{mp['seconds']:.2f} s wall (BASELINE.md B-mp)"}
+            except (subprocess.SubprocessError, OSError, ValueError, KeyError, IndexError) as e:
+                cpu_mp = {"value": None, "error": type(e).__name__}
+        # PCIe-inclusive end-to-end (not `value`): host raster -> pipelined H2D / kernels / D2H -> host frames
         e2e = None
-        if not args.no_e2e:
-            host = np.empty((B, H, W), dtype=dt)
-            ctx.d2h(host, dev_raster)
-            p2 = N.Plan(ctx, host.ctypes.data, False, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"],
-                        keepalive=host)
-            p2.execute()
-            p2.download()
-            reps = 3
-            t0e = time.perf_counter()
-            for _ in range(reps):
-                p2.set_raster(host.ctypes.data, False, keepalive=host)
-                p2.execute()
-                _, fr2 = p2.download()
-            te = (time.perf_counter() - t0e) / reps
-            e2e = {"value": round(my_px / te / 1e6, 2), "unit": "MPix/s", "ms": round(te * 1e3, 2),
-                   "what": "pageable host raster -> H2D -> all kernels -> D2H of all frames (1 GPU)",
-                   "bytes_equal_device_path": bool(fr2 == plan.download()[1])}
-            p2.close()
-            del host
+        if not args.no_e2e and world == 1:
+            if raster_bytes <= (8 << 30):
+                e2e = measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, plan)
+            else:
+                e2e = {"value": None, "note": "skipped by default above 8 GiB of raster (page-locked host copies)"}
         # size vs libFLAC: only pinned for C2 (sample_rgb, 178,857 frame bytes at -c 5)
         size_c2 = None
         try:
@@ -249,6 +419,26 @@ def main():
             size_c2 = round(len(fr) / 178857.0, 5)
         except Exception:
             size_c2 = None
+        # counters of the dominant kernel: in-run passes (this build), else the committed file if current.
+        # The passes run in a child process: release this process's device buffers first.
+        plan.close()
+        ctx.free(dev_raster)
+        plan = dev_raster = None
+        pm = None
+        if not args.no_pmc and world == 1:
+            pm = inrun_pmc(args, dom_name)
+            if "traffic" not in pm and "valu_insts" not in pm:
+                pm = None
+        if pm is None:
+            pm = committed_profile(args, cfg, dom_name)
+        hbm_frac = achieved / HBM_PEAK_GBPS
+        valu_frac = None
+        if pm.get("valu_insts") and pm.get("busy_cycles_per_xcd"):
+            valu_frac = pm["valu_insts"] * VALU_CYC / (SIMDS * pm["busy_cycles_per_xcd"])
+        bound = "hbm" if valu_frac is None or hbm_frac >= valu_frac else "valu"
+        per_rank = [{"rank": k, "ms_per_step": round(r[0] / args.steps * 1e3, 4), "analyze_ms": round(r[1], 4),
+                     "serial_ms": round(r[2], 4), "tiles": int(r[3]), "pixels": int(r[4])} for k, r in enumerate(ranks)]
+        mean_t = sum(r[0] for r in ranks) / len(ranks)
         result = {
             "metric": "raster MPixels/sec encoded at -c 5 + size ratio vs libFLAC, 1/2/4/8 GPU",
             "value": round(value, 2),
@@ -268,26 +458,80 @@ def main():
                        "msamples_per_s": round(job_px * B * args.steps / T / 1e6, 1),
                        "parallelism": (f"{world} scene(s), one per GPU, no collective" if weak else
                                        f"one scene's tiles sharded LPT over {world} GPU(s), no collective"),
-                       "frame_groups": int(os.environ.get("FRA_GROUPS", "1")),
                        "serial_ms_per_step": round(step_ms_local, 4)},
-            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+            "per_rank": per_rank,
+            "imbalance": round(T / mean_t, 4) if mean_t > 0 else None,
+            "roofline": {"bound": bound, "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": pm.get("traffic"),
+                         "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,
+                         "whole_path_frac": round(path_gbps / HBM_PEAK_GBPS, 5),
+                         "whole_path_gbps": round(path_gbps, 2),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "kernel_ms_per_launch": {"minmax": round(per_launch_ms[0], 4),
                                                   "analyze": round(per_launch_ms[1], 4),
                                                   "frame_bytes+scan": round(per_launch_ms[2], 4),
                                                   "pack": round(per_launch_ms[3], 4)},
-                         "whole_path_gbps": round(path_gbps, 2)},
+                         "counters": pm,
+                         "valu_note": f"valu_issue_frac = SQ_INSTS_VALU x {VALU_CYC} cyc / ({SIMDS} SIMDs x "
+                                      "GRBM_GUI_ACTIVE/8) of the same launch"},
             "cpu_baseline": cpu,
+            "cpu_baseline_mp": cpu_mp,
             "size_ratio_vs_libflac_c2": size_c2,
             "e2e": e2e,
         }
         print(json.dumps(result), flush=True)
-    plan.close()
-    ctx.free(dev_raster)
+    if plan is not None:
+        plan.close()
+        ctx.free(dev_raster)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, dev_plan):
+    """Host raster -> frames in host memory through the pipelined ``fra_plan_encode_host`` (row bands:
+    H2D of band b+1 || kernels of band b || D2H of band b-1).  Page-locked buffers (what
+    ``GeoTIFF.read(pinned=True)`` delivers; allocated once, outside the timed region) and, for reference,
+    pageable numpy buffers.  Also the bare PCIe copy times of the same bytes."""
+    host = N.pinned_empty((B, H, W), dt)
+    ctx.d2h(host, dev_raster)
+    plan = N.Plan(ctx, None, False, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
+    cap, nbands = plan.capacity()
+    out = N.pinned_empty(cap, np.uint8)
+    total = plan.encode_host(host, out)  # warm-up
+    ref = dev_plan.download()[1]
+    equal = bytes(out[:total]) == ref
+    del ref
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        total = plan.encode_host(host, out)
+    te = (time.perf_counter() - t0) / reps
+    # bare copies of the same bytes (pinned): the PCIe floor of this path
+    dev_out, _ = plan.device_output()
+    t0 = time.perf_counter()
+    ctx.h2d(dev_raster, host)
+    t_h2d = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    N.load().fra_memcpy_d2h(ctx.h, out.ctypes.data, dev_out, total)
+    t_d2h = time.perf_counter() - t0
+    res = {"value": round(my_px / te / 1e6, 2), "unit": "MPix/s", "ms": round(te * 1e3, 2), "bands": nbands,
+           "what": "page-locked host raster -> pipelined row-band H2D / kernels / D2H -> page-locked host frames (1 GPU)",
+           "bytes_equal_device_path": bool(equal),
+           "h2d_ms_alone": round(t_h2d * 1e3, 2), "d2h_ms_alone": round(t_d2h * 1e3, 2),
+           "pcie_floor_ms": round(max(t_h2d, t_d2h) * 1e3, 2)}
+    # pageable variant (a plain numpy raster and output buffer)
+    hp = np.empty((B, H, W), dt)
+    hp[...] = host
+    op = np.empty(cap, np.uint8)
+    plan.encode_host(hp, op)
+    t0 = time.perf_counter()
+    plan.encode_host(hp, op)
+    tp = time.perf_counter() - t0
+    res["pageable"] = {"value": round(my_px / tp / 1e6, 2), "ms": round(tp * 1e3, 2)}
+    plan.close()
+    del host, out, hp, op
+    return res
 
 
 if __name__ == "__main__":

@@ -108,8 +108,16 @@ struct fra_plan {
   Group all{0, 0, 0, 0};                // the whole plan as one group (timing mode)
   std::vector<hipStream_t> aux;
   std::vector<hipEvent_t> gev;          // [0] start, then per group: offsets-published, done
-  unsigned long long* d_gbase = nullptr;  // [groups + 1] byte offset of each group's first frame
+  unsigned long long* d_gbase = nullptr;  // [max(groups, host bands) + 1] byte offset of each group's first frame
   size_t scan_stride = 0;               // bytes of scan workspace per group
+  // host pipeline (fra_plan_encode_host): row bands of windows; band b copies raster rows [r0, r1)
+  // before its kernels run (rows already copied by earlier bands are not copied again)
+  struct HBand { Group g; int64_t r0, r1; };
+  std::vector<HBand> hbands;
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  std::vector<hipEvent_t> hev;          // per band: rows copied, frames assembled (+ end offset mirrored)
+  hipEvent_t hev_start = nullptr;
+  unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -268,11 +276,69 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_gbase);
   for (auto& st : p->aux)
     if (st) (void)hipStreamDestroy(st);
+  if (p->h2d) (void)hipStreamDestroy(p->h2d);
+  if (p->d2h) (void)hipStreamDestroy(p->d2h);
+  for (auto& e : p->hev)
+    if (e) (void)hipEventDestroy(e);
+  if (p->hev_start) (void)hipEventDestroy(p->hev_start);
+  if (p->h_gbase) (void)hipHostFree(p->h_gbase);
   for (auto& e : p->gev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;
+}
+
+// Row bands for the host pipeline: runs of windows sharing a row offset (a row of tiles), merged until a
+// band holds >= 1/16 of the frames (one band for small plans, where launch latency dominates).  Band b
+// copies the raster rows its windows cover that no earlier band copied; if the windows' row ranges are
+// not monotone the plan falls back to one band covering every row.
+static void build_host_bands(fra_plan* p, int nfr) {
+  p->hbands.clear();
+  const int ns = (int)p->streams.size();
+  if (ns == 0) return;
+  const int64_t min_frames = nfr < 2048 ? (int64_t)nfr + 1 : std::max<int64_t>(1, nfr / 16);
+  std::vector<fra_plan::Group> bands;
+  int w = 0, f = 0;
+  while (w < ns) {
+    fra_plan::Group g{w, w, f, f};
+    while (w < ns && (g.f1 - g.f0 < min_frames || g.w1 == g.w0)) {
+      const int r = p->windows[w].row_off;
+      while (w < ns && p->windows[w].row_off == r) {  // a whole row of windows
+        f += p->streams[w].nframes;
+        w++;
+      }
+      g.w1 = w;
+      g.f1 = f;
+    }
+    bands.push_back(g);
+  }
+  if (bands.size() > 1 && bands.back().f1 - bands.back().f0 < min_frames / 2) {  // fold a small tail band
+    bands[bands.size() - 2].w1 = bands.back().w1;
+    bands[bands.size() - 2].f1 = bands.back().f1;
+    bands.pop_back();
+  }
+  int64_t lo_all = INT64_MAX, hi_all = 0, prev_lo = -1, hi = 0;
+  bool mono = true;
+  for (const auto& g : bands) {
+    int64_t lo = INT64_MAX, hb = 0;
+    for (int k = g.w0; k < g.w1; k++)
+      if (p->streams[k].nsamples > 0) {
+        lo = std::min<int64_t>(lo, p->windows[k].row_off);
+        hb = std::max<int64_t>(hb, (int64_t)p->windows[k].row_off + p->windows[k].height);
+      }
+    if (lo == INT64_MAX) { lo = hi; hb = hi; }
+    if (lo < prev_lo) mono = false;
+    prev_lo = lo;
+    lo_all = std::min(lo_all, lo);
+    hi_all = std::max(hi_all, hb);
+    p->hbands.push_back({g, std::max(lo, hi), std::max(std::max(lo, hi), hb)});
+    hi = std::max(hi, hb);
+  }
+  if (!mono) {
+    p->hbands.clear();
+    p->hbands.push_back({p->all, lo_all == INT64_MAX ? 0 : lo_all, hi_all});
+  }
 }
 
 static int plan_build(fra_plan* p) {
@@ -432,8 +498,11 @@ static int plan_build(fra_plan* p) {
     if (p->groups.empty()) p->groups.push_back(p->all);
     p->groups.back().w1 = (int)p->streams.size();
     p->groups.back().f1 = nfr;
+    build_host_bands(p, nfr);
     size_t mx = 0, tb = 0;
-    for (const auto& gr : p->groups) {
+    std::vector<fra_plan::Group> scan_shapes(p->groups);
+    for (const auto& hb : p->hbands) scan_shapes.push_back(hb.g);
+    for (const auto& gr : scan_shapes) {
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->d_fbytes, p->d_foff, std::max(1, gr.f1 - gr.f0),
                                               p->ctx->stream));
       mx = std::max(mx, tb);
@@ -443,7 +512,7 @@ static int plan_build(fra_plan* p) {
     p->scan_stride = (std::max<size_t>(16, mx) + 255) & ~(size_t)255;
     p->scan_tmp_bytes = p->scan_stride * p->groups.size();
     HIPCHK(hipMalloc(&p->d_scan_tmp, p->scan_tmp_bytes));
-    HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) * (p->groups.size() + 1)));
+    HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) * (std::max(p->groups.size(), p->hbands.size()) + 1)));
     for (size_t g = 1; g < p->groups.size(); g++) {
       hipStream_t st = nullptr;
       HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -559,18 +628,22 @@ static void collect_times(fra_plan* p) {
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
 static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
-                     hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan) {
+                     hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan, int slot = -1) {
   const JobArgs& a = p->args;
   const int nst = gr.w1 - gr.w0, nf = gr.f1 - gr.f0;
-  if (p->job.norm != 0 && nst > 0 && p->max_segs > 0) {
-    JobArgs ma = a;  // the minmax family indexes streams by blockIdx.y: offset to the group's windows
-    ma.streams += gr.w0;
-    ma.norm += gr.w0;
-    if (ma.lut) ma.lut += (int64_t)gr.w0 * a.lut_stride;
+  // the minmax family indexes streams by blockIdx.y: launched per chunk of <= kMaxGridY windows, with the
+  // stream/norm/LUT pointers offset to the chunk (grid Y is limited to 65535 on the device)
+  constexpr int kMaxGridY = 65535;
+  for (int c0 = 0; p->job.norm != 0 && p->max_segs > 0 && c0 < nst; c0 += kMaxGridY) {
+    const int nc = std::min(kMaxGridY, nst - c0);
+    JobArgs ma = a;
+    ma.streams += gr.w0 + c0;
+    ma.norm += gr.w0 + c0;
+    if (ma.lut) ma.lut += (int64_t)(gr.w0 + c0) * a.lut_stride;
     const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
-    HIPCHK(launch_minmax(p->src, ma, nst, p->max_segs, vec, p->mm_rows, p->mm_max_rows, st));
-    HIPCHK(launch_norm_finalize(ma, nst, st));
-    HIPCHK(launch_norm_lut(p->src, ma, nst, st));
+    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, st));
+    HIPCHK(launch_norm_finalize(ma, nc, st));
+    HIPCHK(launch_norm_lut(p->src, ma, nc, st));
   }
   if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
   JobArgs ga = a;
@@ -581,7 +654,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   HIPCHK(launch_frame_bytes(ga, st));
   if (nf > 0) {
     size_t tb = p->scan_stride;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)gi * p->scan_stride, tb,
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)(slot < 0 ? gi : slot) * p->scan_stride, tb,
                                             p->d_fbytes + gr.f0, p->d_foff + gr.f0, nf, st));
   }
   if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
@@ -711,6 +784,133 @@ int fra_plan_timing(fra_plan* p, float* ms4, int32_t* n) {
   collect_times(p);
   for (int k = 0; k < 4; k++) ms4[k] = p->ms[k];
   *n = p->nexec;
+  return FRA_OK;
+}
+
+int fra_plan_capacity(fra_plan* p, uint64_t* capacity, int32_t* host_bands) {
+  if (!p) return set_err(FRA_E_INVALID, "null plan");
+  if (capacity) *capacity = p->out_cap;
+  if (host_bands) *host_bands = (int32_t)p->hbands.size();
+  return FRA_OK;
+}
+
+// H2D of raster rows [r0, r1) of every band (channel) of the job: one contiguous run per channel for
+// band-planar rasters (band_stride >= row_stride), one run for pixel-interleaved ones; clamped to the
+// plan's extent (the last row of the last channel may end before row_stride does)
+static int copy_rows_h2d(fra_plan* p, const uint8_t* host, int64_t r0, int64_t r1, hipStream_t st) {
+  const fra_job& j = p->job;
+  const int es = elem_size(j.dtype);
+  const int64_t extent = (int64_t)(p->raster_bytes / es);
+  const bool planar = j.channels > 1 && j.band_stride >= j.row_stride;
+  const int nrun = planar ? j.channels : 1;
+  for (int c = 0; c < nrun; c++) {
+    const int64_t a = (int64_t)c * (planar ? j.band_stride : 0) + r0 * j.row_stride;
+    const int64_t b = std::min(extent, (int64_t)c * (planar ? j.band_stride : 0) + r1 * j.row_stride);
+    if (b > a)
+      HIPCHK(hipMemcpyAsync((uint8_t*)p->d_raster_owned + a * es, host + a * es, (size_t)(b - a) * es,
+                            hipMemcpyHostToDevice, st));
+  }
+  return FRA_OK;
+}
+
+int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
+                         uint64_t* total_bytes) {
+  if (!p || (!host_raster && p->raster_bytes) || (!host_out && capacity)) return set_err(FRA_E_INVALID, "null argument");
+  (void)hipSetDevice(p->ctx->device);
+  hipStream_t s = p->ctx->stream;
+  const int nb = (int)p->hbands.size();
+  if (total_bytes) *total_bytes = 0;
+  if (nb == 0) {  // no windows
+    p->executed = true;
+    return FRA_OK;
+  }
+  if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
+  p->d_raster = p->d_raster_owned;
+  p->args.raster = p->d_raster;
+  p->job.raster = host_raster;
+  p->job.raster_on_device = 0;
+  p->args.vec8 = (p->ld_vec8 && (uintptr_t)p->d_raster % 8 == 0) ? 1 : 0;
+  if (!p->h2d) HIPCHK(hipStreamCreateWithFlags(&p->h2d, hipStreamNonBlocking));
+  if (!p->d2h) HIPCHK(hipStreamCreateWithFlags(&p->d2h, hipStreamNonBlocking));
+  if (!p->hev_start) HIPCHK(hipEventCreateWithFlags(&p->hev_start, hipEventDisableTiming));
+  if ((int)p->hev.size() < 2 * nb) {
+    for (auto& e : p->hev)
+      if (e) (void)hipEventDestroy(e);
+    p->hev.assign(2 * nb, nullptr);
+    for (auto& e : p->hev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  if (!p->h_gbase) HIPCHK(hipHostMalloc((void**)&p->h_gbase, sizeof(unsigned long long) * (nb + 1), hipHostMallocPortable));
+  // the copies must not overwrite the device raster while earlier work of this plan still reads it
+  HIPCHK(hipEventRecord(p->hev_start, s));
+  HIPCHK(hipStreamWaitEvent(p->h2d, p->hev_start, 0));
+  HIPCHK(hipStreamWaitEvent(p->d2h, p->hev_start, 0));
+  const uint8_t* host = (const uint8_t*)host_raster;
+  auto enqueue_copy = [&](int b) -> int {
+    const auto& hb = p->hbands[b];
+    if (hb.r1 > hb.r0) {
+      const int rc = copy_rows_h2d(p, host, hb.r0, hb.r1, p->h2d);
+      if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(p->hev[2 * b], p->h2d));
+    return FRA_OK;
+  };
+  uint64_t beg = 0;
+  int issued = 0;  // bands whose D2H has been enqueued
+  bool over = false;
+  auto enqueue_d2h = [&](int b) -> int {
+    const uint64_t end = p->h_gbase[b + 1];
+    if (end > capacity) over = true;
+    if (!over && end > beg) {
+      HIPCHK(hipStreamWaitEvent(p->d2h, p->hev[2 * b + 1], 0));
+      HIPCHK(hipMemcpyAsync(host_out + beg, p->d_out + beg, (size_t)(end - beg), hipMemcpyDeviceToHost, p->d2h));
+    }
+    beg = end;
+    return FRA_OK;
+  };
+  int rc = enqueue_copy(0);
+  if (rc) return rc;
+  for (int b = 0; b < nb; b++) {
+    if (b + 1 < nb && (rc = enqueue_copy(b + 1))) return rc;  // the next band's rows go over PCIe meanwhile
+    HIPCHK(hipStreamWaitEvent(s, p->hev[2 * b], 0));
+    rc = run_group(p, p->hbands[b].g, b, nb, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(p->h_gbase + b + 1, p->d_gbase + b + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(p->hev[2 * b + 1], s));
+    // bands already assembled: their D2H can start now (pageable sources make the H2D enqueue blocking)
+    while (issued <= b && hipEventQuery(p->hev[2 * issued + 1]) == hipSuccess)
+      if ((rc = enqueue_d2h(issued++))) return rc;
+  }
+  while (issued < nb) {
+    HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
+    if ((rc = enqueue_d2h(issued++))) return rc;
+  }
+  HIPCHK(hipStreamSynchronize(p->d2h));
+  HIPCHK(hipStreamSynchronize(s));
+  p->executed = true;
+  if (total_bytes) *total_bytes = beg;
+  if (over)
+    return set_err(FRA_E_SPACE, "output needs %llu bytes, capacity %llu (frames stay on the device)",
+                   (unsigned long long)beg, (unsigned long long)capacity);
+  return FRA_OK;
+}
+
+int fra_host_alloc(uint64_t bytes, void** ptr) {
+  if (!ptr) return set_err(FRA_E_INVALID, "null argument");
+  *ptr = nullptr;
+  HIPCHK(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocPortable));
+  return FRA_OK;
+}
+int fra_host_free(void* ptr) {
+  if (ptr) HIPCHK(hipHostFree(ptr));
+  return FRA_OK;
+}
+int fra_host_register(void* ptr, uint64_t bytes) {
+  if (!ptr || !bytes) return set_err(FRA_E_INVALID, "null argument");
+  HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+  return FRA_OK;
+}
+int fra_host_unregister(void* ptr) {
+  if (ptr) HIPCHK(hipHostUnregister(ptr));
   return FRA_OK;
 }
 

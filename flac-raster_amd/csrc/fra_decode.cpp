@@ -215,6 +215,9 @@ bool read_subframe(Bits& br, int n, int bps, int64_t* s, std::vector<int32_t>& r
   if (br.get(1)) wasted = (int)br.unary() + 1;
   if (wasted >= bps) return false;
   const int eb = bps - wasted;
+  // reconstructed samples must fit the subframe's sample width (libFLAC rejects such frames too);
+  // keeping every s[] within eb <= 33 bits also bounds the predictor sums below 2^53: no int64 overflow
+  const int64_t lo = -((int64_t)1 << (eb - 1)), hi = ((int64_t)1 << (eb - 1)) - 1;
   if (type == 0) {
     const int64_t v = br.sget_wide(eb);
     if (write) for (int i = 0; i < n; i++) s[i] = v;
@@ -242,6 +245,7 @@ bool read_subframe(Bits& br, int n, int bps, int64_t* s, std::vector<int32_t>& r
           case 4: p = 4 * s[i - 1] - 6 * s[i - 2] + 4 * s[i - 3] - s[i - 4]; break;
         }
         s[i] = p + res[i];
+        if (s[i] < lo || s[i] > hi) return false;
       }
     }
   } else if (type >= 32) {
@@ -264,6 +268,7 @@ bool read_subframe(Bits& br, int n, int bps, int64_t* s, std::vector<int32_t>& r
         int64_t acc = 0;
         for (int j = 0; j < order; j++) acc += (int64_t)coef[j] * s[i - 1 - j];
         s[i] = (acc >> shift) + res[i];
+        if (s[i] < lo || s[i] > hi) return false;
       }
     }
   } else {
@@ -319,7 +324,7 @@ size_t decode_frame(const uint8_t* p, const uint8_t* end, const StreamParams& sp
 
 // "fLaC" + metadata blocks; returns the offset of the first audio byte (0 on error)
 size_t parse_metadata(const uint8_t* d, size_t len, size_t at, StreamParams& sp) {
-  if (len - at < 8 || memcmp(d + at, "fLaC", 4) != 0) return 0;
+  if (at > len || len - at < 8 || memcmp(d + at, "fLaC", 4) != 0) return 0;
   size_t q = at + 4;
   bool have_si = false;
   for (;;) {
@@ -364,6 +369,8 @@ FRA_API int fra_decode(const uint8_t* data, uint64_t len, int32_t flags, fra_dec
   if (len >= 10 && memcmp(data, "ID3", 3) == 0) {  // ID3v2 prefix (mutagen may leave one)
     at = 10 + (((size_t)data[6] & 0x7F) << 21 | ((size_t)data[7] & 0x7F) << 14 | ((size_t)data[8] & 0x7F) << 7 |
                ((size_t)data[9] & 0x7F));
+    if (at > len) return fra_internal_set_error(FRA_E_INVALID, "ID3v2 tag (%llu bytes) runs past the end of the data",
+                                                (unsigned long long)at);
   }
   StreamParams sp;
   size_t audio = parse_metadata(data, len, at, sp);

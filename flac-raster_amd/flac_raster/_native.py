@@ -33,6 +33,12 @@ class NativeError(RuntimeError):
     pass
 
 
+class OutputTooSmall(NativeError):
+    def __init__(self, needed: int):
+        super().__init__(f"output buffer too small: {needed} bytes needed")
+        self.needed = needed
+
+
 class Window(C.Structure):
     _fields_ = [("row_off", C.c_int32), ("col_off", C.c_int32), ("height", C.c_int32), ("width", C.c_int32)]
 
@@ -61,6 +67,20 @@ class Decoded(C.Structure):
 
 
 DECODE_CONCAT = 1
+E_SPACE = -6
+
+
+class TiffChunk(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("bytes", C.c_uint64), ("row0", C.c_int32), ("col0", C.c_int32),
+                ("rows", C.c_int32), ("cols", C.c_int32), ("plane", C.c_int32), ("pad", C.c_int32)]
+
+
+class TiffLayout(C.Structure):
+    _fields_ = [("compression", C.c_int32), ("predictor", C.c_int32), ("bytes_per_sample", C.c_int32),
+                ("samples_per_pixel", C.c_int32), ("is_float", C.c_int32), ("big_endian", C.c_int32),
+                ("bands", C.c_int32), ("win_row", C.c_int32), ("win_col", C.c_int32), ("win_h", C.c_int32),
+                ("win_w", C.c_int32), ("pad", C.c_int32), ("dst_band_stride", C.c_int64),
+                ("dst_row_stride", C.c_int64)]
 
 EXPORTS = [
     "fra_last_error", "fra_abi_version", "fra_device_count", "fra_free", "fra_ctx_create", "fra_ctx_destroy",
@@ -68,7 +88,8 @@ EXPORTS = [
     "fra_plan_download", "fra_plan_device_output", "fra_plan_enable_timing", "fra_plan_timing",
     "fra_plan_destroy", "fra_encode", "fra_stream_header", "fra_synth_raster", "fra_device_alloc",
     "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d", "fra_plan_frame_offsets", "fra_normalize",
-    "fra_decode",
+    "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
+    "fra_host_register", "fra_host_unregister", "fra_tiff_decode",
 ]
 
 
@@ -115,6 +136,13 @@ def load():
         pd = C.POINTER(C.c_double)
         L.fra_normalize.argtypes = [vp, vp, i32, i32, u64, i32, pd, pd, vp, pd, pd]
         L.fra_decode.argtypes = [vp, u64, i32, C.POINTER(Decoded), C.POINTER(C.POINTER(C.c_int32))]
+        L.fra_plan_encode_host.argtypes = [vp, vp, vp, u64, C.POINTER(u64)]
+        L.fra_plan_capacity.argtypes = [vp, C.POINTER(u64), C.POINTER(i32)]
+        L.fra_host_alloc.argtypes = [u64, C.POINTER(vp)]
+        L.fra_host_free.argtypes = [vp]
+        L.fra_host_register.argtypes = [vp, u64]
+        L.fra_host_unregister.argtypes = [vp]
+        L.fra_tiff_decode.argtypes = [vp, u64, C.POINTER(TiffLayout), C.POINTER(TiffChunk), i32, vp, i32]
         _lib = L
         return L
 
@@ -135,6 +163,94 @@ def stream_header(channels: int, bps: int, sample_rate: int, blocksize: int = 40
     buf = (C.c_uint8 * 86)()
     _check(load().fra_stream_header(buf, channels, bps, sample_rate, blocksize))
     return bytes(buf)
+
+
+_PIN_POOL_BYTES = int(os.environ.get("FRA_PINNED_POOL_MB", "8192")) << 20
+_pin_pool: List[Tuple[int, int]] = []  # (capacity, ptr) of released page-locked blocks kept for reuse
+_pin_lock = threading.Lock()
+
+
+class _PinnedBlock:
+    """Owner of one page-locked host allocation (``fra_host_alloc``), exposed to numpy.  Released blocks
+    go to a small pool (``FRA_PINNED_POOL_MB``, default 8 GiB) because pinning pages costs far more than
+    copying through them; the pool reuses a block of at most twice the requested size."""
+
+    def __init__(self, nbytes: int):
+        nbytes = max(1, int(nbytes))
+        ptr, cap = None, 0
+        with _pin_lock:
+            best = None
+            for k, (c, p) in enumerate(_pin_pool):
+                if nbytes <= c <= 2 * nbytes and (best is None or c < _pin_pool[best][0]):
+                    best = k
+            if best is not None:
+                cap, ptr = _pin_pool.pop(best)
+        if ptr is None:
+            p = C.c_void_p()
+            _check(load().fra_host_alloc(nbytes, C.byref(p)))
+            ptr, cap = p.value, nbytes
+        self.ptr = ptr
+        self.capacity = cap
+        self.nbytes = nbytes
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        try:
+            if not self.ptr:
+                return
+            ptr, self.ptr = self.ptr, None
+            with _pin_lock:
+                pooled = sum(c for c, _ in _pin_pool)
+                if pooled + self.capacity <= _PIN_POOL_BYTES:
+                    _pin_pool.append((self.capacity, ptr))
+                    return
+            load().fra_host_free(C.c_void_p(ptr))
+        except Exception:
+            pass
+
+
+def release_pinned_pool():
+    """Free every pooled page-locked block."""
+    with _pin_lock:
+        blocks = list(_pin_pool)
+        _pin_pool.clear()
+    for _, p in blocks:
+        load().fra_host_free(C.c_void_p(p))
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """``np.empty`` in page-locked host memory (full-rate PCIe DMA; freed with the array).  Needs the
+    HIP runtime (a GPU box); raises :class:`NativeError` without one."""
+    dt = np.dtype(dtype)
+    shape = (shape,) if isinstance(shape, int) else tuple(shape)
+    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    return np.asarray(_PinnedBlock(n)).view(dt)[: n // dt.itemsize].reshape(shape)
+
+
+def is_pinned(a: np.ndarray) -> bool:
+    base = a
+    while base is not None and not isinstance(base, _PinnedBlock):
+        base = getattr(base, "base", None)
+    return base is not None
+
+
+class HostRegistration:
+    """``hipHostRegister`` of an existing host array for the lifetime of a ``with`` block."""
+
+    def __init__(self, a: np.ndarray):
+        self.a = a
+        self.ok = False
+
+    def __enter__(self):
+        if self.a.nbytes and not is_pinned(self.a):
+            _check(load().fra_host_register(C.c_void_p(self.a.ctypes.data), self.a.nbytes))
+            self.ok = True
+        return self.a
+
+    def __exit__(self, *exc):
+        if self.ok:
+            load().fra_host_unregister(C.c_void_p(self.a.ctypes.data))
+            self.ok = False
 
 
 class Context:
@@ -241,6 +357,27 @@ class Plan:
         _check(load().fra_plan_download(self.h, buf.ctypes.data_as(C.c_void_p), total))
         return infos, buf[:total].tobytes()
 
+    def capacity(self) -> Tuple[int, int]:
+        """(upper bound of the output bytes, number of host-pipeline row bands)."""
+        cap, nb = C.c_uint64(), C.c_int32()
+        _check(load().fra_plan_capacity(self.h, C.byref(cap), C.byref(nb)))
+        return cap.value, nb.value
+
+    def encode_host(self, raster: np.ndarray, out: np.ndarray) -> int:
+        """Pipelined host raster -> host frames (``fra_plan_encode_host``): row bands of the raster go
+        H2D while earlier bands are analysed, and each band's frames come back D2H as soon as they are
+        assembled.  ``raster`` must have the plan's dtype/strides; ``out`` is a uint8 buffer (page-locked
+        for full rate).  Returns the total frame bytes; raises :class:`OutputTooSmall` (with ``.needed``)
+        if ``out`` is too small -- the frames then stay on the device (``download``)."""
+        total = C.c_uint64()
+        self._keep = raster
+        rc = load().fra_plan_encode_host(self.h, C.c_void_p(raster.ctypes.data), C.c_void_p(out.ctypes.data),
+                                         out.nbytes, C.byref(total))
+        if rc == E_SPACE:
+            raise OutputTooSmall(total.value)
+        _check(rc)
+        return total.value
+
     def frame_offsets(self, nframes: int) -> np.ndarray:
         """Byte offset of every frame in the concatenated output (+ total at the end)."""
         off = np.empty(nframes + 1, dtype=np.uint64)
@@ -286,13 +423,53 @@ def default_context(device: int = 0) -> Context:
     return ctx
 
 
+def _element_strides(a: np.ndarray) -> Tuple[int, int, int]:
+    es = a.dtype.itemsize
+    if any(st < 0 or st % es for st in a.strides):
+        raise ValueError("raster strides must be non-negative multiples of the item size")
+    return tuple(st // es for st in a.strides)
+
+
+def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize: int = 4096, norm: int = 16,
+                          sample_rate: int = 0, device: int = 0, pinned: bool = True):
+    """Encode windows of a band-planar host raster ``(B, H, W)`` (any non-negative strides, e.g. a row
+    band view of a larger raster) through the pipelined host path (``fra_plan_encode_host``).
+
+    Returns ``(infos, frames)``: ``frames`` is a uint8 array (page-locked unless ``pinned=False``) with
+    every window's FLAC frames concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.
+    """
+    a = np.asarray(raster)
+    if a.ndim == 2:
+        a = a[None]
+    if a.dtype not in DTYPE_CODES:
+        raise TypeError(f"unsupported dtype {a.dtype}")
+    if not a.dtype.isnative:
+        a = a.astype(a.dtype.newbyteorder("="))
+    B = a.shape[0]
+    ctx = default_context(device)
+    plan = Plan(ctx, None, False, a.dtype, B, _element_strides(a), windows, level, blocksize, norm, sample_rate)
+    try:
+        cap, _ = plan.capacity()
+        out = pinned_empty(cap, np.uint8) if pinned else np.empty(cap, np.uint8)
+        total = plan.encode_host(a, out)
+        infos, _ = plan.result()
+        return infos, out[:total]
+    finally:
+        plan.close()
+
+
 def encode_windows(raster: np.ndarray, windows, level: int = 5, blocksize: int = 4096, norm: int = 16,
-                   sample_rate: int = 0, device: int = 0):
+                   sample_rate: int = 0, device: int = 0, path: str = "host"):
     """Encode windows of a band-planar host raster ``(B, H, W)`` (or ``(H, W)``).
 
     Returns ``(infos, frames_bytes)``: ``frames_bytes`` holds every window's FLAC frames
-    concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.
+    concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.  ``path="host"`` is the
+    pipelined host path (``fra_plan_encode_host``); ``path="device"`` copies the whole raster first and
+    runs ``fra_plan_execute`` (frame groups per ``FRA_GROUPS``) then ``fra_plan_download``.
     """
+    if path == "host":
+        infos, buf = encode_windows_buffer(raster, windows, level, blocksize, norm, sample_rate, device)
+        return infos, buf.tobytes()
     a = np.ascontiguousarray(raster)
     if a.ndim == 2:
         a = a[None]

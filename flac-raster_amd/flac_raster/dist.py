@@ -5,11 +5,19 @@ the data path.  The only collective is the final hand-off of the encoded streams
 writes the container (``gather_streams``), plus barrier / max-time reductions for measurement.
 Works with ``torch.distributed`` on ``nccl`` (= RCCL over xGMI on MI355X) or ``gloo`` (CPU tests);
 launched by ``torch.distributed.run`` (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR in the env).
+
+The compressed streams never travel through RCCL: each rank copies its frames D2H (the pipelined
+``fra_plan_encode_host``) and writes them to a node-local spool file (``/dev/shm``); only a small
+manifest (tile ids, lengths, min/max) goes through a gloo group, and the writer rank reads the spool.
+Ranks on other hosts (no shared spool) send their bytes through the gloo group instead.
 """
 
 from __future__ import annotations
 
 import os
+import socket
+import tempfile
+from pathlib import Path
 from typing import Callable, List, Optional, Sequence, Tuple
 
 from .tiles import TileStream, encode_tiles, lpt_assign
@@ -23,6 +31,7 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
+        self.host_pg = None  # gloo group for host-side hand-offs (None: the default group is gloo)
         if self.world > 1:
             import torch
             import torch.distributed as td
@@ -34,6 +43,8 @@ class Dist:
             if not td.is_initialized():
                 td.init_process_group(backend=backend)
             self.pg = td
+            if backend != "gloo":
+                self.host_pg = td.new_group(backend="gloo")
         self.backend = backend
 
     def _dev(self):
@@ -60,7 +71,57 @@ class Dist:
         if self.pg is None:
             return [obj]
         out = [None] * self.world if self.rank == dst else None
-        self.pg.gather_object(obj, out, dst=dst)
+        self.pg.gather_object(obj, out, dst=dst, group=self.host_pg)
+        return out
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.pg is None:
+            return obj
+        box = [obj]
+        self.pg.broadcast_object_list(box, src=src, group=self.host_pg)
+        return box[0]
+
+    def gather_streams(self, items: List[Tuple[int, TileStream]], dst: int = 0):
+        """Hand every rank's ``(tile id, TileStream)`` list to ``dst`` (others get ``None``) through a
+        node-local spool file per rank; only the manifest goes through the (gloo) process group."""
+        if self.pg is None:
+            return [items]
+        host = socket.gethostname()
+        spool = None
+        if self.rank == dst:
+            shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+            spool = tempfile.mkdtemp(prefix="fra_gather_", dir=shm)
+        dst_host, spool = self.broadcast_object((host, spool), src=dst)
+        meta = [(i, len(ts.header), len(ts.body), ts.data_min, ts.data_max, ts.sample_rate, ts.bps, ts.channels,
+                 ts.nframes) for i, ts in items]
+        if host == dst_host:
+            path = os.path.join(spool, f"rank{self.rank}.bin")
+            with open(path, "wb") as f:
+                for _, ts in items:
+                    f.write(ts.header)
+                    f.write(ts.body)
+            payload = ("file", path, meta)
+        else:  # no shared spool: bytes through the gloo group
+            payload = ("inline", b"".join(ts.header + bytes(ts.body) for _, ts in items), meta)
+        parts = self.gather_objects(payload, dst)
+        if self.rank != dst:
+            return None
+        out = []
+        for kind, where, man in parts:
+            if kind == "file":
+                buf = Path(where).read_bytes()
+                os.unlink(where)
+            else:
+                buf = where
+            mv, pos, lst = memoryview(buf), 0, []
+            for (i, hl, bl, mn, mx, sr, bps, ch, nf) in man:
+                lst.append((i, TileStream(bytes(mv[pos:pos + hl]), mv[pos + hl:pos + hl + bl], mn, mx, sr, bps, ch, nf)))
+                pos += hl + bl
+            out.append(lst)
+        try:
+            os.rmdir(spool)
+        except OSError:
+            pass
         return out
 
     def close(self):
@@ -86,7 +147,7 @@ def encode_tiles_distributed(raster, tiles: Sequence[Tuple[int, int, int, int]],
     d = d or Dist()
     mine = shard(tiles, d.world, d.rank)
     streams = encode_fn(raster, [tiles[i] for i in mine], level, [d.local_rank]) if mine else []
-    parts = d.gather_objects(list(zip(mine, streams)), dst)
+    parts = d.gather_streams(list(zip(mine, streams)), dst)
     if d.rank != dst:
         return None
     out: List[Optional[TileStream]] = [None] * len(tiles)

@@ -132,9 +132,10 @@ def default_padding(available_minus_needed: int, audio_bytes: int) -> int:
     return low
 
 
-def rewrite_header(data: bytes, tags: Sequence[Tuple[str, str]], clear: bool = True) -> bytes:
-    """``FLAC(f); f.clear(); f[k] = v ...; f.save()`` on the bytes of a file -> new bytes."""
-    blocks, audio_off = parse_blocks(data, 0)
+def rewrite_header_parts(header: bytes, audio_bytes: int, tags: Sequence[Tuple[str, str]], clear: bool = True) -> bytes:
+    """The new metadata part (``fLaC`` + blocks + PADDING) of ``rewrite_header`` for a file whose metadata
+    is ``header`` and whose audio is ``audio_bytes`` long (the audio itself is not needed)."""
+    blocks, audio_off = parse_blocks(header, 0)
     kept: List[Tuple[int, bytes]] = []
     vc = None
     for bt, body in blocks:
@@ -157,9 +158,15 @@ def rewrite_header(data: bytes, tags: Sequence[Tuple[str, str]], clear: bool = T
         out += render_block(bt, vc.render() if bt == VORBIS_COMMENT else body, False)
     available = audio_off - 4
     needed = len(out) + 4
-    pad = max(default_padding(available - needed, len(data) - audio_off), 0)
+    pad = max(default_padding(available - needed, audio_bytes), 0)
     out += render_block(PADDING, bytes(pad), True)
-    return b"fLaC" + bytes(out) + data[audio_off:]
+    return b"fLaC" + bytes(out)
+
+
+def rewrite_header(data: bytes, tags: Sequence[Tuple[str, str]], clear: bool = True) -> bytes:
+    """``FLAC(f); f.clear(); f[k] = v ...; f.save()`` on the bytes of a file -> new bytes."""
+    _, audio_off = parse_blocks(data, 0)
+    return rewrite_header_parts(data[:audio_off], len(data) - audio_off, tags, clear) + data[audio_off:]
 
 
 class FLACFile:

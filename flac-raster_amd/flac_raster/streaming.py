@@ -27,37 +27,52 @@ from .tiff import GeoTIFF
 from .tiles import TileStream, calculate_tiles, encode_tiles
 
 
-def tile_flac_bytes(ts: TileStream, transform: Affine, crs: Optional[str], row_off: int, col_off: int, height: int,
-                    width: int, dtype) -> Tuple[bytes, Affine]:
-    """One tile's file as ``converter.tiff_to_flac(temp_tile.tif)`` would write it."""
+def tile_flac_parts(ts: TileStream, transform: Affine, crs: Optional[str], row_off: int, col_off: int, height: int,
+                    width: int, dtype):
+    """One tile's file as ``converter.tiff_to_flac(temp_tile.tif)`` would write it, as (tagged metadata
+    bytes, frames view, window transform): the frames are not copied."""
     tt = window_transform(transform, col_off, row_off)
     md = raster_metadata(width, height, ts.channels, dtype, crs, tt, ts.data_min, ts.data_max, None,
                          32767 if ts.bps == 16 else 8388607)
-    return flac_meta.rewrite_header(ts.data, raster_tags(md)), tt
+    return flac_meta.rewrite_header_parts(ts.header, len(ts.body), raster_tags(md)), ts.body, tt
 
 
-def assemble_streaming(tiles: Sequence[Tuple[int, int, int, int]], streams: Sequence[TileStream], shape,
-                       dtype, transform: Affine, crs: Optional[str], tile_size: int) -> bytes:
-    """Container bytes from encoded tile streams (tile order = ``calculate_tiles`` order)."""
+def tile_flac_bytes(ts: TileStream, transform: Affine, crs: Optional[str], row_off: int, col_off: int, height: int,
+                    width: int, dtype) -> Tuple[bytes, Affine]:
+    head, body, tt = tile_flac_parts(ts, transform, crs, row_off, col_off, height, width, dtype)
+    return head + bytes(body), tt
+
+
+def streaming_parts(tiles: Sequence[Tuple[int, int, int, int]], streams: Sequence[TileStream], shape, dtype,
+                    transform: Affine, crs: Optional[str], tile_size: int) -> List:
+    """The container as a list of bytes-like parts (index first); frames stay zero-copy views."""
     B, H, W = shape
     index: Dict = {"crs": str(crs), "transform": list(transform), "width": W, "height": H, "bands": B,
                    "dtype": str(np.dtype(dtype)), "tile_size": tile_size, "frames": []}
-    chunks: List[bytes] = []
+    parts: List = []
     total = 0
     for fid, ((r, c, h, w), ts) in enumerate(zip(tiles, streams)):
-        data, tt = tile_flac_bytes(ts, transform, crs, r, c, h, w, dtype)
+        head, body, tt = tile_flac_parts(ts, transform, crs, r, c, h, w, dtype)
+        size = len(head) + len(body)
         xmin, ymax = tt.c, tt.f
         index["frames"].append({
             "frame_id": fid,
             "bbox": [xmin, ymax + h * tt.e, xmin + w * tt.a, ymax],
             "window": {"col_off": c, "row_off": r, "width": w, "height": h},
             "byte_offset": total,
-            "byte_size": len(data),
+            "byte_size": size,
         })
-        chunks.append(data)
-        total += len(data)
+        parts += [head, body]
+        total += size
     head = json.dumps(index, separators=(",", ":")).encode("utf-8")
-    return len(head).to_bytes(4, "big") + head + b"".join(chunks)
+    return [len(head).to_bytes(4, "big") + head] + parts
+
+
+def assemble_streaming(tiles: Sequence[Tuple[int, int, int, int]], streams: Sequence[TileStream], shape,
+                       dtype, transform: Affine, crs: Optional[str], tile_size: int) -> bytes:
+    """Container bytes from encoded tile streams (tile order = ``calculate_tiles`` order)."""
+    return b"".join(bytes(p) if isinstance(p, memoryview) else p
+                    for p in streaming_parts(tiles, streams, shape, dtype, transform, crs, tile_size))
 
 
 def build_streaming(raster: np.ndarray, transform: Affine, crs: Optional[str], tile_size: int,
@@ -71,12 +86,22 @@ def build_streaming(raster: np.ndarray, transform: Affine, crs: Optional[str], t
 
 def create_streaming_flac(input_path: Path, output_path: Path, tile_size: int = 512, compression_level: int = 5,
                           devices: Optional[Sequence[int]] = None) -> Dict:
-    """Write the streaming container for a GeoTIFF; returns the index."""
+    """Write the streaming container for a GeoTIFF; returns the index.
+
+    The raster is decoded straight into page-locked memory (``GeoTIFF.read(pinned=True)``), encoded by
+    the pipelined host path (row bands H2D while earlier bands are analysed, frames D2H per band) and
+    the container is written from zero-copy views of the page-locked frames."""
     g = GeoTIFF(input_path)
-    raster = g.read()
-    out = build_streaming(raster, Affine(*g.info.transform), g.info.crs, tile_size, compression_level, devices)
-    Path(output_path).write_bytes(out)
-    return read_index_bytes(out)[0]
+    raster = g.read(pinned=True)
+    tiles = calculate_tiles(raster.shape[1], raster.shape[2], tile_size)
+    streams = encode_tiles(raster, tiles, compression_level, devices)
+    parts = streaming_parts(tiles, streams, raster.shape, raster.dtype, Affine(*g.info.transform), g.info.crs,
+                            tile_size)
+    with open(output_path, "wb") as f:
+        for p in parts:
+            f.write(p)
+    n = struct.unpack(">I", parts[0][:4])[0]
+    return json.loads(parts[0][4:4 + n].decode("utf-8"))
 
 
 @dataclass

@@ -6,7 +6,8 @@ The reference reads rasters with ``rasterio.open(...).read()`` (``converter.py:7
 subset the encode path needs:
 
 * baseline TIFF + BigTIFF, II/MM byte order, strips or tiles, PlanarConfiguration 1 or 2,
-  Compression 1 (none), 8 (Adobe deflate), 32946 (deflate); Predictor 1/2 for integers;
+  Compression 1 (none), 5 (LZW), 8 (Adobe deflate), 32946 (deflate); Predictor 1, 2 (integers),
+  3 (floating point) -- decoded natively (``csrc/fra_tiff.cpp``), any other value is rejected;
 * SampleFormat uint / int / IEEE float, 8/16/32/64 bits;
 * GeoTIFF ModelPixelScale + ModelTiepoint or ModelTransformation -> affine transform
   (GDAL order ``(a, b, c, d, e, f)`` as ``list(rasterio.Affine)[:6]``), GeoKeyDirectory -> ``EPSG:n``.
@@ -16,8 +17,9 @@ Arrays are returned band-planar ``(bands, height, width)`` like ``rasterio.read(
 
 from __future__ import annotations
 
+import mmap
+import os
 import struct
-import zlib
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Optional
@@ -58,11 +60,22 @@ def _dtype_from(fmt: int, bits: int) -> np.dtype:
 
 
 class GeoTIFF:
-    """Read-only GeoTIFF.  ``read()`` -> (bands, H, W); ``read_window(r, c, h, w)``."""
+    """Read-only GeoTIFF.  ``read()`` -> (bands, H, W); ``read_window(r, c, h, w)``.
+
+    The file is memory-mapped; only the IFD is parsed in Python.  Strips/tiles are decoded by the
+    native multi-threaded decoder (``fra_tiff_decode``: none / LZW / deflate, predictors 1-3) straight
+    into the destination array -- page-locked memory when ``pinned=True`` (the layout the pipelined
+    encode ``fra_plan_encode_host`` copies at full PCIe rate).  A window read decodes only the chunks
+    that overlap the window (rasterio ``read(window=...)``, ``cli.py:559``).
+    """
 
     def __init__(self, path):
         self.path = Path(path)
-        self._buf = self.path.read_bytes()
+        with open(self.path, "rb") as f:
+            size = os.fstat(f.fileno()).st_size
+            if size < 8:
+                raise ValueError(f"not a TIFF: {path}")
+            self._buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
         b = self._buf
         if b[:2] == b"II":
             self.bo = "<"
@@ -84,10 +97,16 @@ class GeoTIFF:
         spp = int(t.get(277, [1])[0])
         bits = t.get(258, [8] * spp)
         fmt = int(t.get(339, [1])[0])
+        if any(int(x) != int(bits[0]) for x in bits) or int(bits[0]) not in (8, 16, 32, 64):
+            raise NotImplementedError(f"TIFF BitsPerSample {bits} not supported")
         self.dtype = _dtype_from(fmt, int(bits[0])).newbyteorder(self.bo)
         self.planar = int(t.get(284, [1])[0])
         self.compression = int(t.get(259, [1])[0])
         self.predictor = int(t.get(317, [1])[0])
+        if self.compression not in (1, 5, 8, 32946):
+            raise NotImplementedError(f"TIFF compression {self.compression} not supported (none, LZW, deflate)")
+        if self.predictor not in (1, 2, 3) or (self.predictor == 2 and fmt == 3) or (self.predictor == 3 and fmt != 3):
+            raise NotImplementedError(f"TIFF predictor {self.predictor} not supported for SampleFormat {fmt}")
         transform = (1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
         if 34264 in t:
             m = t[34264]
@@ -114,6 +133,23 @@ class GeoTIFF:
                 nodata = None
         self.info = RasterInfo(W, H, spp, np.dtype(self.dtype.newbyteorder("=")), transform, crs, nodata, {})
         self._data = None
+        # chunk grid
+        self.tiled = 322 in t
+        self._offs = t[324] if self.tiled else t[273]
+        self._cnts = t[325] if self.tiled else t[279]
+        if self.tiled:
+            self.cw, self.ch = int(t[322][0]), int(t[323][0])
+        else:
+            self.cw, self.ch = W, int(t.get(278, [H])[0])
+        self.nx = (W + self.cw - 1) // self.cw
+        self.ny = (H + self.ch - 1) // self.ch
+
+    def close(self):
+        if self._buf is not None:
+            try:
+                self._buf.close()
+            except BufferError:  # still exported to a live array
+                pass
 
     # -- IFD parsing
     def _read_ifd(self, off: int) -> dict:
@@ -149,60 +185,85 @@ class GeoTIFF:
                 tags[tag] = list(struct.unpack(bo + _TYPE_FMT.get(typ, "B") * cnt, data))
         return tags
 
-    def _decode_chunk(self, raw: bytes) -> bytes:
-        if self.compression == 1:
-            return raw
-        if self.compression in (8, 32946):
-            return zlib.decompress(raw)
-        raise NotImplementedError(f"TIFF compression {self.compression} not supported")
+    def _chunks(self, row_off: int, col_off: int, height: int, width: int):
+        """Strips/tiles overlapping the window, as ``fra_tiff_chunk`` records."""
+        from . import _native as N
 
-    def read(self) -> np.ndarray:
-        """All bands, (count, H, W) native-endian -- rasterio ``read()`` equivalent."""
-        if self._data is not None:
-            return self._data
-        t, info = self.tags, self.info
-        W, H, S = info.width, info.height, info.count
-        dt = self.dtype
-        out = np.empty((S, H, W), dtype=dt.newbyteorder("="))
-        tiled = 322 in t
-        offs = t[324] if tiled else t[273]
-        cnts = t[325] if tiled else t[279]
-        if tiled:
-            tw, th = int(t[322][0]), int(t[323][0])
-        else:
-            tw, th = W, int(t.get(278, [H])[0])
-        nx = (W + tw - 1) // tw
-        ny = (H + th - 1) // th
-        per_plane = nx * ny
-        planes = S if self.planar == 2 else 1
-        spc = 1 if self.planar == 2 else S
+        H = self.info.height
+        cy0, cy1 = row_off // self.ch, (row_off + height - 1) // self.ch
+        cx0, cx1 = col_off // self.cw, (col_off + width - 1) // self.cw
+        planes = self.info.count if self.planar == 2 else 1
+        per_plane = self.nx * self.ny
+        out = []
         for pl in range(planes):
-            for cy in range(ny):
-                for cx in range(nx):
-                    idx = pl * per_plane + cy * nx + cx
-                    raw = self._buf[offs[idx]:offs[idx] + cnts[idx]]
-                    dec = self._decode_chunk(raw)
-                    rows = th if tiled else min(th, H - cy * th)
-                    arr = np.frombuffer(dec, dtype=dt, count=rows * tw * spc).reshape(rows, tw, spc)
-                    if self.predictor == 2:
-                        arr = np.cumsum(arr, axis=1, dtype=arr.dtype)
-                    r0, c0 = cy * th, cx * tw
-                    r1, c1 = min(r0 + rows, H), min(c0 + tw, W)
-                    blk = arr[: r1 - r0, : c1 - c0, :]
-                    if self.planar == 2:
-                        out[pl, r0:r1, c0:c1] = blk[:, :, 0]
-                    else:
-                        out[:, r0:r1, c0:c1] = np.moveaxis(blk, 2, 0)
-        self._data = out
+            for cy in range(cy0, cy1 + 1):
+                for cx in range(cx0, cx1 + 1):
+                    idx = pl * per_plane + cy * self.nx + cx
+                    rows = self.ch if self.tiled else min(self.ch, H - cy * self.ch)
+                    out.append(N.TiffChunk(int(self._offs[idx]), int(self._cnts[idx]), cy * self.ch, cx * self.cw,
+                                           rows, self.cw, pl, 0))
         return out
 
-    def read_window(self, row_off: int, col_off: int, height: int, width: int) -> np.ndarray:
-        return self.read()[:, row_off:row_off + height, col_off:col_off + width]
+    def read_window_into(self, out: np.ndarray, row_off: int, col_off: int, height: int, width: int,
+                         threads: int = 0) -> np.ndarray:
+        """Decode a window into ``out`` (band-planar ``(bands, height, width)`` view, native byte order,
+        unit column stride; e.g. a page-locked array from ``_native.pinned_empty``)."""
+        import ctypes as C
+
+        from . import _native as N
+
+        info = self.info
+        if out.shape != (info.count, height, width) or out.dtype != info.dtype:
+            raise ValueError(f"out must be {(info.count, height, width)} {info.dtype}, got {out.shape} {out.dtype}")
+        es = info.dtype.itemsize
+        if out.strides[2] != es or out.strides[0] % es or out.strides[1] % es:
+            raise ValueError("out needs unit column stride")
+        if not (0 <= row_off and 0 <= col_off and row_off + height <= info.height and col_off + width <= info.width):
+            raise ValueError("window outside the raster")
+        if height == 0 or width == 0:
+            return out
+        chunks = self._chunks(row_off, col_off, height, width)
+        arr = (N.TiffChunk * len(chunks))(*chunks)
+        lay = N.TiffLayout(self.compression, self.predictor, es, 1 if self.planar == 2 else info.count,
+                           1 if info.dtype.kind == "f" else 0, 1 if self.bo == ">" else 0, info.count, row_off,
+                           col_off, height, width, 0, out.strides[0] // es, out.strides[1] // es)
+        src = np.frombuffer(self._buf, dtype=np.uint8)
+        N._check(N.load().fra_tiff_decode(src.ctypes.data_as(C.c_void_p), len(self._buf), C.byref(lay), arr,
+                                          len(chunks), out.ctypes.data_as(C.c_void_p), threads))
+        del src
+        return out
+
+    def read(self, out: Optional[np.ndarray] = None, pinned: bool = False) -> np.ndarray:
+        """All bands, (count, H, W) native-endian -- rasterio ``read()`` equivalent."""
+        info = self.info
+        if out is None:
+            if self._data is not None and not pinned:
+                return self._data
+            out = _alloc((info.count, info.height, info.width), info.dtype, pinned)
+            self.read_window_into(out, 0, 0, info.height, info.width)
+            if not pinned:
+                self._data = out
+            return out
+        return self.read_window_into(out, 0, 0, info.height, info.width)
+
+    def read_window(self, row_off: int, col_off: int, height: int, width: int, pinned: bool = False) -> np.ndarray:
+        """rasterio ``read(window=Window(col_off, row_off, width, height))``: only the overlapping chunks
+        are decoded."""
+        out = _alloc((self.info.count, height, width), self.info.dtype, pinned)
+        return self.read_window_into(out, row_off, col_off, height, width)
 
 
-def read_geotiff(path):
+def _alloc(shape, dtype, pinned: bool) -> np.ndarray:
+    if pinned:
+        from . import _native as N
+
+        return N.pinned_empty(shape, dtype)
+    return np.empty(shape, dtype=dtype)
+
+
+def read_geotiff(path, pinned: bool = False):
     g = GeoTIFF(path)
-    return g.read(), g.info
+    return g.read(pinned=pinned), g.info
 
 
 def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = None, nodata=None):

@@ -64,15 +64,31 @@ def lpt_assign(weights: Sequence[int], parts: int) -> List[List[int]]:
 
 @dataclass
 class TileStream:
-    """One encoded unit: a complete FLAC stream (86-byte header + frames) + its normalisation."""
+    """One encoded unit: a complete FLAC stream (86-byte header + frames) + its normalisation.
 
-    data: bytes
+    ``header`` is the 86-byte libFLAC-layout header, ``body`` the frames -- a zero-copy view into the
+    page-locked output of the pipelined encode (``_native.encode_windows_buffer``); ``data`` joins them."""
+
+    header: bytes
+    body: object  # bytes-like (memoryview / bytes)
     data_min: float
     data_max: float
     sample_rate: int
     bps: int        # FLAC bits per sample (16, or 32 for int32 audio: SURVEY.md F3)
     channels: int
     nframes: int
+
+    @property
+    def data(self) -> bytes:
+        return self.header + bytes(self.body)
+
+    def __len__(self) -> int:
+        return len(self.header) + len(self.body)
+
+    def __getstate__(self):  # pickling (multi-process gather) materialises the view
+        st = dict(self.__dict__)
+        st["body"] = bytes(self.body)
+        return st
 
 
 def norm_bits(dtype) -> int:
@@ -85,17 +101,16 @@ def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]]
     try:
         r0 = min(t[0] for t in tiles)
         r1 = max(t[0] + t[2] for t in tiles)
-        sub = raster if (r0 == 0 and r1 == raster.shape[1]) else np.ascontiguousarray(raster[:, r0:r1, :])
+        sub = raster[:, r0:r1, :]  # a view: the plan copies only these rows, band by band
         wins = [(t[0] - r0, t[1], t[2], t[3]) for t in tiles]
-        infos, frames = _native.encode_windows(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
-                                               device=device)
+        infos, frames = _native.encode_windows_buffer(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
+                                                      device=device)
         res = []
         mv = memoryview(frames)
         for inf in infos:
             hdr = _native.stream_header(inf.channels, inf.bps, inf.sample_rate, BLOCKSIZE)
-            body = mv[inf.offset:inf.offset + inf.frame_bytes]
-            res.append(TileStream(hdr + bytes(body), float(inf.data_min), float(inf.data_max), inf.sample_rate,
-                                  inf.bps, inf.channels, inf.nframes))
+            res.append(TileStream(hdr, mv[inf.offset:inf.offset + inf.frame_bytes], float(inf.data_min),
+                                  float(inf.data_max), inf.sample_rate, inf.bps, inf.channels, inf.nframes))
         out[slot] = res
     except BaseException as e:  # re-raised on the calling thread
         errors.append(e)
@@ -111,6 +126,8 @@ def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]],
     a = np.asarray(raster)
     if a.ndim == 2:
         a = a[None]
+    if not a.dtype.isnative:
+        a = a.astype(a.dtype.newbyteorder("="))
     if a.dtype not in _native.DTYPE_CODES:
         raise TypeError(f"unsupported raster dtype {a.dtype}")
     if not tiles:

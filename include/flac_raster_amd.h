@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define FRA_ABI_VERSION 1
+#define FRA_ABI_VERSION 2
 
 #if defined(__GNUC__) || defined(__clang__)
 #define FRA_API __attribute__((visibility("default")))
@@ -53,7 +53,8 @@ typedef enum {
   FRA_E_HIP = -2,       /* HIP runtime error (message in fra_last_error) */
   FRA_E_NODEVICE = -3,  /* no usable gfx950 device */
   FRA_E_NOMEM = -4,
-  FRA_E_STATE = -5      /* call out of order (e.g. result before execute) */
+  FRA_E_STATE = -5,     /* call out of order (e.g. result before execute) */
+  FRA_E_SPACE = -6      /* caller's output buffer too small (the required size is reported) */
 } fra_status;
 
 /* dtype codes of the source samples (numpy names) */
@@ -121,6 +122,27 @@ FRA_API int fra_plan_enable_timing(fra_plan *plan, int32_t on);
 FRA_API int fra_plan_timing(fra_plan *plan, float *ms_sum4, int32_t *executes);
 FRA_API void fra_plan_destroy(fra_plan *plan);
 
+/* Host-resident raster -> host-resident frames in one pipelined pass (the PCIe-inclusive path that
+ * replaces rasterio read -> pyflac encode -> file write per tile, cli.py:553-602 / converter.py:73-154).
+ * The windows are grouped into row bands; the raster rows of band b are copied H2D on a copy stream
+ * while the kernels of band b-1 run on the plan's stream, and band b's frames are copied D2H on a
+ * second copy stream as soon as they are assembled (PCIe is full duplex).  host_raster has the job's
+ * dtype and strides; host_raster and host_out should be page-locked (fra_host_alloc/fra_host_register)
+ * for full link rate.  Frames land at the offsets fra_plan_result reports; *total_bytes = their sum.
+ * If capacity < total, FRA_E_SPACE is returned (frames beyond capacity are not copied; the complete
+ * output stays on the device for fra_plan_download).  Synchronous: returns when the frames are in
+ * host_out.  A plan's capacity bound: fra_plan_capacity. */
+FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
+                                 uint64_t *total_bytes);
+/* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
+FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
+
+/* page-locked host memory (hipHostMalloc / hipHostRegister, portable across devices) */
+FRA_API int fra_host_alloc(uint64_t bytes, void **host_ptr);
+FRA_API int fra_host_free(void *host_ptr);
+FRA_API int fra_host_register(void *host_ptr, uint64_t bytes);
+FRA_API int fra_host_unregister(void *host_ptr);
+
 /* One-shot convenience: plan, execute, download.  *out (malloc'ed, fra_free) receives the
  * concatenated frames; infos must hold job->nwindows entries. */
 FRA_API int fra_encode(int device, const fra_job *job, uint8_t **out, uint64_t *out_len, fra_stream_info *infos);
@@ -160,6 +182,34 @@ FRA_API int fra_decode(const uint8_t *data, uint64_t len, int32_t flags, fra_dec
  * uint16 (4 bands), 5 = C5 reflectance float32.  dev_out: device buffer (bands, height, width). */
 FRA_API int fra_synth_raster(fra_ctx *ctx, int32_t kind, uint64_t seed, int32_t bands, int32_t height, int32_t width,
                      void *dev_out);
+
+/* GeoTIFF chunk decoder (host, multi-threaded; raster I/O ahead of the path, SURVEY.md 8(f) f3,
+ * replacing rasterio's window reads at cli.py:559 / converter.py:73-79 / spatial_encoder.py:205-206).
+ * The caller parses the IFD and lists the strips/tiles overlapping the window; each is decompressed
+ * (none, LZW, deflate), un-predicted (1, 2 horizontal, 3 floating point) and its overlap with the
+ * window written band-planar into dst (element (b, r, c) of the window at
+ * b*dst_band_stride + r*dst_row_stride + c, native byte order).  threads <= 0: hardware concurrency. */
+typedef struct {
+  uint64_t offset, bytes;   /* compressed chunk within the file buffer */
+  int32_t row0, col0;       /* image position of the chunk's first pixel */
+  int32_t rows, cols;       /* chunk extent as stored (full tile, or strip rows x image width) */
+  int32_t plane;            /* band of a planar (PlanarConfiguration 2) chunk; ignored when chunky */
+  int32_t pad;
+} fra_tiff_chunk;
+typedef struct {
+  int32_t compression;        /* 1, 5 (LZW), 8 or 32946 (deflate) */
+  int32_t predictor;          /* 1, 2, 3 */
+  int32_t bytes_per_sample;   /* 1, 2, 4, 8 */
+  int32_t samples_per_pixel;  /* per chunk: SamplesPerPixel when chunky, 1 when planar */
+  int32_t is_float;           /* SampleFormat 3 */
+  int32_t big_endian;         /* MM file */
+  int32_t bands;              /* bands of the destination */
+  int32_t win_row, win_col, win_h, win_w;  /* destination window in image pixels */
+  int32_t pad;
+  int64_t dst_band_stride, dst_row_stride; /* elements */
+} fra_tiff_layout;
+FRA_API int fra_tiff_decode(const uint8_t *file, uint64_t file_len, const fra_tiff_layout *layout,
+                            const fra_tiff_chunk *chunks, int32_t nchunks, void *dst, int32_t threads);
 
 /* device memory helpers for hosts without a GPU array library */
 FRA_API int fra_device_alloc(fra_ctx *ctx, uint64_t bytes, void **dev_ptr);

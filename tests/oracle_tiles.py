@@ -22,6 +22,6 @@ def oracle_encode_tiles(raster, tiles, level=5, devices=None):
         audio, mn, mx = O.normalize(inter, bps_norm)
         sr = O.sample_rate_for_pixels(h * w)
         data = O.encode(audio, sr, level=level)
-        out.append(TileStream(data, float(mn), float(mx), sr, 16 if bps_norm == 16 else 32, B,
+        out.append(TileStream(data[:86], data[86:], float(mn), float(mx), sr, 16 if bps_norm == 16 else 32, B,
                               (h * w + 4095) // 4096))
     return out

@@ -185,9 +185,9 @@ def test_frame_groups_pipelined_equal_serial(monkeypatch, groups):
     r = synth_window(3, 21, 1, H, W)
     wins = tiles(H, W, 512) + [(0, 0, 0, 0)]  # an empty window in the last group
     monkeypatch.setenv("FRA_GROUPS", "1")
-    i1, f1 = N.encode_windows(r, wins, level=5, norm=16)
+    i1, f1 = N.encode_windows(r, wins, level=5, norm=16, path="device")
     monkeypatch.setenv("FRA_GROUPS", str(groups))
-    ig, fg = N.encode_windows(r, wins, level=5, norm=16)
+    ig, fg = N.encode_windows(r, wins, level=5, norm=16, path="device")
     assert fg == f1
     assert [(a.offset, a.frame_bytes, a.nframes) for a in ig] == [(a.offset, a.frame_bytes, a.nframes) for a in i1]
     check_windows(r, [wins[0], wins[len(wins) // 2], wins[-2]], 5, 16)

@@ -1,0 +1,105 @@
+"""GPU tests of the PCIe-inclusive path: fra_plan_encode_host (row bands: H2D of band
+b+1 || kernels of band b || D2H of band b-1) must give exactly the bytes and stream table of the
+device-resident path, for page-locked and pageable buffers, strided raster views, non-monotone window
+orders (single-band fallback) and a too-small output buffer; and GeoTIFFs in the compressions GDAL
+writes (LZW, deflate, predictors 2 and 3) must reach the same container bytes as the oracle."""
+import numpy as np
+import pytest
+
+from flac_raster import _native as N
+from flac_raster.geo import Affine
+from flac_raster.streaming import assemble_streaming, create_streaming_flac
+from flac_raster.synth import synth_window
+from flac_raster.tiles import calculate_tiles
+from oracle_tiles import oracle_encode_tiles
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_path(r, wins, level, norm):
+    return N.encode_windows(r, wins, level=level, norm=norm, path="device")
+
+
+def _table(infos):
+    return [(i.offset, i.frame_bytes, i.nframes, i.sample_rate, i.data_min, i.data_max) for i in infos]
+
+
+@pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm", [
+    (3, 1, 4096, 4096, 512, np.int16, 5, 16),      # C3-like: 8 row bands
+    (4, 4, 3600, 3600, 1024, np.uint16, 5, 16),    # C4-like: ragged edge tiles
+    (5, 3, 1536, 1536, 512, np.float32, 8, 24),    # C5-like: 32-bps
+])
+def test_encode_host_equals_device_path(kind, bands, H, W, tile, dtype, level, norm):
+    r = synth_window(kind, 41, bands, H, W).astype(dtype)
+    wins = calculate_tiles(H, W, tile)
+    di, df = _device_path(r, wins, level, norm)
+    plan = N.Plan(N.default_context(0), None, False, r.dtype, bands, (H * W, W, 1), wins, level, 4096, norm)
+    try:
+        cap, nbands = plan.capacity()
+        assert nbands > 1
+        pin = N.pinned_empty(r.shape, r.dtype)
+        pin[...] = r
+        out = N.pinned_empty(cap, np.uint8)
+        total = plan.encode_host(pin, out)
+        infos, _ = plan.result()
+        assert bytes(out[:total]) == df and _table(infos) == _table(di)
+        page = np.empty(cap, np.uint8)  # pageable raster and output
+        assert plan.encode_host(r, page) == total and bytes(page[:total]) == df
+        small = np.empty(total // 2, np.uint8)  # too small: FRA_E_SPACE, frames stay on the device
+        with pytest.raises(N.OutputTooSmall) as e:
+            plan.encode_host(pin, small)
+        assert e.value.needed == total
+        assert plan.download()[1] == df
+    finally:
+        plan.close()
+
+
+def test_encode_host_strided_view_and_window_orders():
+    r = synth_window(4, 8, 3, 2600, 2200)
+    view = r[:, 300:2600, :]  # a row band of a larger raster: strides stay those of r
+    wins = calculate_tiles(2300, 2200, 512)
+    exp_i, exp_f = _device_path(np.ascontiguousarray(view), wins, 5, 16)
+    gi, gf = N.encode_windows_buffer(view, wins, 5, 4096, 16)
+    assert bytes(gf) == exp_f and _table(gi) == _table(exp_i)
+    rev = wins[::-1]  # non-monotone row order -> one band covering every row
+    ri, rf = N.encode_windows(view, rev, 5, 4096, 16)
+    di, df = _device_path(np.ascontiguousarray(view), rev, 5, 16)
+    assert rf == df and _table(ri) == _table(di)
+
+
+def _gdal_like_tiff(path, a, compression, predictor):
+    """Strip GeoTIFF written by an independent libtiff (Pillow) -- single band, as Pillow supports."""
+    from PIL import Image
+
+    kw = {"compression": compression}
+    if predictor != 1:
+        kw["tiffinfo"] = {317: predictor}
+    Image.fromarray(a[0]).save(path, **kw)
+
+
+@pytest.mark.parametrize("compression,predictor,dtype,level,tile", [
+    ("tiff_lzw", 2, np.uint16, 5, 512),
+    ("tiff_lzw", 1, np.uint16, 5, 384),
+    ("tiff_adobe_deflate", 2, np.uint16, 5, 512),
+    ("tiff_adobe_deflate", 3, np.float32, 8, 256),
+])
+def test_compressed_geotiff_to_streaming_container(tmp_path, compression, predictor, dtype, level, tile):
+    pytest.importorskip("PIL")
+    r = synth_window(4 if dtype == np.uint16 else 5, 3, 1, 1100, 1300).astype(dtype)
+    p = tmp_path / "in.tif"
+    _gdal_like_tiff(p, r, compression, predictor)
+    out = tmp_path / "s.flac"
+    create_streaming_flac(p, out, tile, level)
+    tiles = calculate_tiles(1100, 1300, tile)
+    ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, level), r.shape, r.dtype,
+                             Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0), None, tile)
+    assert out.read_bytes() == ref
+
+
+def test_pinned_pool_reuse():
+    a = N.pinned_empty(1 << 20, np.uint8)
+    p = a.ctypes.data
+    del a
+    b = N.pinned_empty((1 << 20) - 100, np.uint8)
+    assert b.ctypes.data == p and N.is_pinned(b)
+    N.release_pinned_pool()

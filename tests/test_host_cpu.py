@@ -48,7 +48,7 @@ def test_abi_exports_every_declared_symbol():
     missing = [s for s in sorted(decl) if not hasattr(L, s)]
     assert not missing, missing
     assert set(N.EXPORTS) == decl
-    assert L.fra_abi_version() == 1
+    assert L.fra_abi_version() == 2
 
 
 def test_abi_errors_without_device():
@@ -84,6 +84,51 @@ def test_decoder_rejects_corruption_and_truncation(golden_dir):
         N.decode(bytes(d[:-100]))
     with pytest.raises(N.NativeError):
         N.decode(b"RIFF0000")
+
+
+def test_decoder_rejects_id3_past_end():
+    """an ID3v2 size pointing past the buffer must fail cleanly, not read out of bounds."""
+    with pytest.raises(N.NativeError):
+        N.decode(b"ID3\x04\x00\x00\x7f\x7f\x7f\x7f" + b"fLaC")
+    with pytest.raises(N.NativeError):
+        N.decode(b"ID3\x04\x00\x00\x00\x00\x00\x05fL")
+
+
+def _crc(data, poly, width):
+    c = 0
+    top = 1 << (width - 1)
+    mask = (1 << width) - 1
+    for b in data:
+        c ^= b << (width - 8)
+        for _ in range(8):
+            c = ((c << 1) ^ poly) & mask if c & top else (c << 1) & mask
+    return c
+
+
+def test_decoder_rejects_out_of_range_prediction():
+    """a CRC-valid frame whose FIXED reconstruction leaves the 16-bit sample range is
+    rejected (libFLAC does too) instead of overflowing / truncating."""
+    hdr = N.stream_header(1, 16, 44100, 16)
+    bits = []
+
+    def put(v, n):
+        bits.extend((v >> (n - 1 - i)) & 1 for i in range(n))
+    # frame header: sync, fixed blocksize, bs code 6 (8-bit bs-1), sr 44.1k, mono, 16 bit, frame 0
+    put(0xFFF8, 16); put(6, 4); put(9, 4); put(0, 4); put(4, 3); put(0, 1); put(0, 8); put(15, 8)
+    fh = bytes(int("".join(map(str, bits[i:i + 8])), 2) for i in range(0, len(bits), 8))
+    bits.clear()
+    # FIXED order 1, warm-up 32767, residual partition order 0 escaped to 17-bit raw residuals of 65535
+    put(0, 1); put(9, 6); put(0, 1); put(32767, 16)
+    put(0, 2); put(0, 4); put(15, 4); put(17, 5)
+    for _ in range(15):
+        put(65535, 17)
+    while len(bits) % 8:
+        bits.append(0)
+    body = bytes(int("".join(map(str, bits[i:i + 8])), 2) for i in range(0, len(bits), 8))
+    frame = fh + bytes([_crc(fh, 0x07, 8)]) + body
+    frame += _crc(frame, 0x8005, 16).to_bytes(2, "big")
+    with pytest.raises(N.NativeError):
+        N.decode(hdr + frame)
 
 
 def test_decoder_concatenated_streams(golden_dir):
