@@ -95,8 +95,11 @@ struct AnalyzeSmem {
   typename std::conditional<B32, int32_t, int16_t>::type smp[kSmpWords];
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
-    uint32_t buf[buf_words<B32>()];                 // encoded subframe (big-endian words, MSB first)
+    // encoded subframe (big-endian words, MSB first).  32-bps path: the buffer aliases smp, dead once
+    // the winner's residuals are in registers (keeps the workgroup at <= 40 KiB: 4 per CU, not 3)
+    uint32_t buf[B32 ? 1 : buf_words<B32>()];
   } u;
+  int32_t warm[kMaxLpc];  // 32-bps path: warm-up samples, saved before smp is reused as the bit buffer
   union {
     unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
     struct {  // after the model search (node is dead): winner's exact-pass sums / Rice parameters
@@ -1048,6 +1051,7 @@ read_x28(S.smp, t, x);
       uu[jj] = (i < n && i >= o) ? uv : 0u;
     }
   }
+  if (B32 && t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the decision
   __syncthreads();
   {
     const int pz = n >> ps;
@@ -1150,10 +1154,33 @@ read_x28(S.smp, t, x);
   const int ftype = S.ftype;
   const uint32_t fbits = S.fbits;
   const uint32_t nw = (fbits + 31) >> 5;
-  uint32_t* buf = S.u.buf;
+  const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
+  if constexpr (B32) {
+    if (ftype == 1) {
+      // VERBATIM (rare): each output word assembled from the <= 3 samples it covers, straight from smp
+      // to the slot (smp is still intact: the aliased bit buffer is not touched on this path)
+      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+      const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
+      for (uint32_t j = t; j < nw; j += kThreads) {
+        const int64_t wb = 32 * (int64_t)j;
+        uint32_t word = j == 0 ? (uint32_t)(hv >> 32) : (j == 1 ? (uint32_t)hv : 0u);
+        int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
+        for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
+          const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
+          const int sft = 32 - (int)rel - sbps;
+          const uint64_t v = (uint64_t)((uint32_t)S.smp[sidx(s)] & smask);
+          word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
+        }
+        slot[j] = word;
+      }
+      return;
+    }
+  }
+  // 32-bps path: every smp read (the winner's residuals, the warm-up copy) precedes the decision barrier
+  uint32_t* buf = B32 ? reinterpret_cast<uint32_t*>(S.smp) : S.u.buf;
+  static_assert(!B32 || sizeof(S.smp) >= sizeof(uint32_t) * (buf_words<true>() + 1), "bit buffer inside smp");
   for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
   __syncthreads();
-  const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
   if (t == 0) {
     const int tcode = ftype == 1 ? 1 : ftype == 2 ? 8 + o : 31 + o;
     lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
@@ -1163,7 +1190,8 @@ read_x28(S.smp, t, x);
     for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
   } else {
     const int pb = S.fmethod ? 5 : 4;
-    for (int i = t; i < o; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
+    for (int i = t; i < o; i += kThreads)
+      lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)(B32 ? S.warm[i] : (int32_t)S.smp[sidx(i)]) & smask, sbps);
     uint32_t pos = hdr + (uint32_t)o * sbps;
     if (ftype == 3) {
       if (t == 0) {

@@ -36,7 +36,7 @@ hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
-                                hipStream_t s);
+                                hipStream_t s, unsigned long long* host_mirror = nullptr);
 hipError_t launch_synth(int kind, uint64_t seed, int bands, int H, int W, void* out, hipStream_t s);
 hipError_t launch_normalize_flat(int src, const void* data, uint64_t n, int bps, NormDev* nd, int has_min, double omin,
                                  int has_max, double omax, void* out, hipStream_t s);
@@ -118,6 +118,7 @@ struct fra_plan {
   std::vector<hipEvent_t> hev;          // per band: rows copied, frames assembled (+ end offset mirrored)
   hipEvent_t hev_start = nullptr;
   unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
+  unsigned long long* d_gbase_mirror = nullptr;  // its device address
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -628,7 +629,8 @@ static void collect_times(fra_plan* p) {
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
 static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
-                     hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan, int slot = -1) {
+                     hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan, int slot = -1,
+                     unsigned long long* host_mirror = nullptr) {
   const JobArgs& a = p->args;
   const int nst = gr.w1 - gr.w0, nf = gr.f1 - gr.f0;
   // the minmax family indexes streams by blockIdx.y: launched per chunk of <= kMaxGridY windows, with the
@@ -659,7 +661,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   }
   if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
   HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
-                              a.nframes_total, st));
+                              a.nframes_total, st, host_mirror));
   if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
   if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
   HIPCHK(launch_assemble(ga, st));
@@ -839,7 +841,14 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
     p->hev.assign(2 * nb, nullptr);
     for (auto& e : p->hev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  if (!p->h_gbase) HIPCHK(hipHostMalloc((void**)&p->h_gbase, sizeof(unsigned long long) * (nb + 1), hipHostMallocPortable));
+  if (!p->h_gbase) {
+    HIPCHK(hipHostMalloc((void**)&p->h_gbase, sizeof(unsigned long long) * (nb + 1),
+                         hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&p->d_gbase_mirror, p->h_gbase, 0));
+  }
+  // experiment knobs (defaults = measured best): FRA_H2D_AHEAD bands of H2D ahead of the oldest band whose
+  // D2H is not yet issued (0 = unlimited; 1 measured best on C4: 21.3 vs 22.2 ms)
+  static const int ahead = getenv("FRA_H2D_AHEAD") ? atoi(getenv("FRA_H2D_AHEAD")) : 1;
   // the copies must not overwrite the device raster while earlier work of this plan still reads it
   HIPCHK(hipEventRecord(p->hev_start, s));
   HIPCHK(hipStreamWaitEvent(p->h2d, p->hev_start, 0));
@@ -870,11 +879,18 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
   int rc = enqueue_copy(0);
   if (rc) return rc;
   for (int b = 0; b < nb; b++) {
-    if (b + 1 < nb && (rc = enqueue_copy(b + 1))) return rc;  // the next band's rows go over PCIe meanwhile
+    if (b + 1 < nb) {  // the next band's rows go over PCIe meanwhile
+      while (ahead > 0 && b + 1 - issued > ahead) {
+        HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
+        if ((rc = enqueue_d2h(issued++))) return rc;
+      }
+      if ((rc = enqueue_copy(b + 1))) return rc;
+    }
     HIPCHK(hipStreamWaitEvent(s, p->hev[2 * b], 0));
-    rc = run_group(p, p->hbands[b].g, b, nb, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+    // the band's end offset reaches h_gbase by a kernel store (k_group_offsets), not by a copy-engine
+    // command that would queue behind the H2D copies
+    rc = run_group(p, p->hbands[b].g, b, nb, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p->d_gbase_mirror);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(p->h_gbase + b + 1, p->d_gbase + b + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(p->hev[2 * b + 1], s));
     // bands already assembled: their D2H can start now (pageable sources make the H2D enqueue blocking)
     while (issued <= b && hipEventQuery(p->hev[2 * issued + 1]) == hipSuccess)

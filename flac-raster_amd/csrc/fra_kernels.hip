@@ -274,7 +274,8 @@ hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
 // gbase[grp] (written by the previous group's launch, ordered by an event) is the byte offset of the
 // group's first frame.  Adds it, publishes gbase[grp + 1] and, for the last group, frame_off[nframes].
 __global__ void k_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
-                                unsigned long long* gbase, int grp, int f0, int n, int last, int nframes) {
+                                unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
+                                unsigned long long* host_mirror) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned long long base = grp == 0 ? 0ull : gbase[grp];
   if (i < n) {
@@ -284,18 +285,26 @@ __global__ void k_group_offsets(unsigned long long* frame_off, const unsigned lo
       const unsigned long long end = base + loc + frame_bytes[f0 + i];
       gbase[grp + 1] = end;
       if (last) frame_off[nframes] = end;
+      if (host_mirror) {  // page-locked host copy for the host pipeline (no copy-engine command needed)
+        host_mirror[grp + 1] = end;
+        __threadfence_system();
+      }
     }
   } else if (i == 0) {  // empty group
     gbase[grp + 1] = base;
     if (last) frame_off[nframes] = base;
+    if (host_mirror) {
+      host_mirror[grp + 1] = base;
+      __threadfence_system();
+    }
   }
 }
 
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
-                                hipStream_t s) {
+                                hipStream_t s, unsigned long long* host_mirror) {
   k_group_offsets<<<((n > 1 ? n : 1) + 255) / 256, 256, 0, s>>>(frame_off, frame_bytes, gbase, grp, f0, n, last,
-                                                              nframes);
+                                                              nframes, host_mirror);
   return hipGetLastError();
 }
 

@@ -200,3 +200,20 @@ def test_minmax_one_vector_wide_windows():
         r = synth_window(3, 5, 2, 96, 64).astype(dt)
         wins = [(0, 0, 96, 32), (0, 64 - w, 96, w), (32, 32, 64, w)]
         check_windows(r, wins, 5, 16)
+
+
+@pytest.mark.parametrize("blocksize", [4096, 1000])
+def test_32bps_verbatim_and_wasted_bits(blocksize):
+    """32-bps VERBATIM subframes (full-range noise, also with wasted bits) and partial frames: the
+    32-bps encoder writes VERBATIM words straight from the sample buffer (its bit buffer aliases it)."""
+    rng = np.random.default_rng(blocksize)
+    n = 3 * 4096 + 1234
+    full = rng.integers(-2**31, 2**31, size=(n, 2), dtype=np.int64).astype(np.int32)
+    wasted = (rng.integers(-2**26, 2**26, size=(n, 2)) << 5).astype(np.int32)
+    mixed = rng.integers(-3000, 3000, size=(n, 2)).astype(np.int32)
+    mixed[::97] = rng.integers(-2**30, 2**30, size=mixed[::97].shape)
+    for a in (full, wasted, mixed):
+        info, frames = N.encode_interleaved(a, 44100, level=8, blocksize=blocksize)
+        assert frames == O.encode(a, 44100, level=8, blocksize=blocksize, with_header=False)
+        dec, _, _, _ = O.decode(O.stream_header(2, 32, 44100, blocksize) + frames)
+        assert np.array_equal(dec, a)

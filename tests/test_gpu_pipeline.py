@@ -27,7 +27,7 @@ def _table(infos):
 @pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm", [
     (3, 1, 4096, 4096, 512, np.int16, 5, 16),      # C3-like: 8 row bands
     (4, 4, 3600, 3600, 1024, np.uint16, 5, 16),    # C4-like: ragged edge tiles
-    (5, 3, 1536, 1536, 512, np.float32, 8, 24),    # C5-like: 32-bps
+    (5, 3, 3072, 3072, 512, np.float32, 8, 24),    # C5-like: 32-bps
 ])
 def test_encode_host_equals_device_path(kind, bands, H, W, tile, dtype, level, norm):
     r = synth_window(kind, 41, bands, H, W).astype(dtype)
