@@ -81,12 +81,9 @@ __device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)
   }
 }
 
-// windows per block at this lag bound (levels 3-6: <= 3 with max_lpc 8; levels 7-8: <= 6) and the
-// waves that run Levinson-Durbin (window wi on wave wi % 4)
+// windows per block at this lag bound (levels 3-6: <= 3 with max_lpc 8; levels 7-8: <= 6)
 template <int MAXLAG>
 constexpr int kWinCap() { return MAXLAG == 0 ? 1 : (MAXLAG <= 8 ? 3 : kMaxWin); }
-template <int MAXLAG>
-constexpr int kLdWaves() { return kWinCap<MAXLAG>() < 4 ? kWinCap<MAXLAG>() : 4; }
 
 template <bool B32, int MAXLAG>
 struct AnalyzeSmem {
@@ -109,13 +106,13 @@ struct AnalyzeSmem {
     } e;
   } nu;
   double red[kWinCap<MAXLAG>()][4][MAXLAG + 1];  // per window, per wave: reduced chunk partials
-  double lp[kLdWaves<MAXLAG>()][MAXLAG > 0 ? MAXLAG : 1][MAXLAG > 0 ? MAXLAG : 1];  // LD rows per LD wave
+  double lp[kWinCap<MAXLAG>()][MAXLAG > 0 ? lp_row(MAXLAG) : 1];  // LD rows per window (triangular)
   int32_t mcoef[kMaxModels][kMaxLpc];
   int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
   // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
   // partition order (written by porder_search, read by the winner's exact pass)
-  uint8_t kbest[B32 ? 1 : kMaxModels][kMaxPart];
+  uint8_t kbest[kMaxModels][kMaxPart];
   uint32_t ired[4][3];
   uint32_t scan[4];
   int32_t winner, ftype, fmethod;
@@ -335,6 +332,28 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
   }
 }
 
+// VERBATIM subframe written word by word straight to its slot (32-bps path, whose LDS bit buffer aliases
+// the sample array): word j = the <= 3 samples (sbps >= 16 bits... any sbps >= 1) overlapping bits
+// [32 j, 32 j + 32) of header (8 + w bits) + samples, MSB first -- the words lds_put would produce
+template <typename SmpT>
+__device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t nw,
+                                 int t) {
+  const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
+  const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
+  for (uint32_t j = t; j < nw; j += kThreads) {
+    const int64_t wb = 32 * (int64_t)j;
+    uint32_t word = j == 0 ? (uint32_t)(hv >> 32) : (j == 1 ? (uint32_t)hv : 0u);
+    const int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
+    for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
+      const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
+      const int sft = 32 - (int)rel - sbps;
+      const uint64_t v = (uint64_t)((uint32_t)smp[sidx(s)] & smask);
+      word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
+    }
+    slot[j] = word;
+  }
+}
+
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
@@ -431,11 +450,15 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_an
   // this thread's 16 (samples past n are never counted: their sums/codes are masked by i0 < n / i < n)
   int32_t x[12 + kChunk];
   const bool fastframe = (psz % kChunk) == 0;  // uniform: each thread's 16 samples in one partition
+  // FIXED sums by 32-bit finite differences (v_sad_u32): every 16-bit block, and 32-bps blocks whose
+  // samples stay within +-2^23 (normalize_to_audio's 24-bit range): |4th difference| < 2^27, so 16 of
+  // them fit 32 bits and no residual leaves int32 -- the same integers as the 64-bit sums
+  const bool fixfast = fastframe && (!B32 || (vmin > -(1 << 23) && vmax < (1 << 23)));
   const bool head = i0 == 0;                    // this thread holds the warm-up samples (order <= 12 < 16)
   const int pidx0 = i0 < n ? i0 / psz : 0;
   const int nmod = 5 + (MAXLAG > 0 ? a.nwin : 0);
-  if (!B32 && fastframe) {
-read_x28(S.smp, t, x);
+  if (fixfast) {
+    read_x28(S.smp, t, x);
     // FIXED 0..4 by finite differences, in place: after step k, x[j] for j >= 8 + k holds the
     // k-th difference; |4th difference| < 2^20, so 16 zig-zags fit 32 bits.  Same integers as the
     // oracle's closed forms; every fixed model is valid here (n >= 16).
@@ -461,7 +484,7 @@ read_x28(S.smp, t, x);
   FRA_STOP(9)
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
-  const bool early = !B32 && fastframe && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
+  const bool early = fixfast && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
 
   // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window
   float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
@@ -537,139 +560,77 @@ read_x28(S.smp, t, x);
       }
       __syncthreads();
       FRA_STOP(8)
-      if constexpr (MAXLAG <= 8) {
-        // levels 3-6 (<= 3 windows): the two FIXED candidates on waves 1-2 while wave 0 runs the
-        // Levinson-Durbin of EVERY window at once, window w on lanes 16w..16w+15 (the same op sequence
-        // per lane: one window's instruction cost for all three) -> expected bits of order o on lane
-        // 16w+o -> first minimum per lane group -> qlp quantisation per group
-        if (early && (wv == 1 || wv == 2)) {
-          int g1, g2;
-          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
-          if (wv == 1 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
-          const int m = wv == 1 ? g1 : g2;
-          if (m >= 0) {
-            const int pm = max_porder(n, m, cfg.max_porder);
-            uint64_t best = 0;
-            int bp = pm;
-            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
-            if (lane == 0) {
-              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
-              S.mporder[m] = bp;
-            }
-          }
-        }
-        if (wv == 0) {
-          const int gw = lane >> 4, lo = lane & 15;
-          const bool gon = gw < a.nwin;
-          const int ws = gon ? gw : 0;
-          double ac[MAXLAG + 1];
-#pragma unroll
-          for (int l = 0; l <= MAXLAG; l++)
-            ac[l] = l <= lmax ? (S.red[ws][0][l] + S.red[ws][1][l]) + (S.red[ws][2][l] + S.red[ws][3][l]) : 0.0;
-          int nord = 0;
-          double errv[MAXLAG];
-          if (gon && ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[ws], errv, lo == 0);
-          double e = errv[0];
-#pragma unroll
-          for (int j = 1; j < MAXLAG; j++)
-            if (lo == j + 1) e = errv[j];
-          // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as an
-          // unsigned integer; DPP min inside each 16-lane row (lane 15 of the row), lowest lane among
-          // the equal ones
-          const bool on = nord > 0 && lo >= 1 && lo <= nord;
-          const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lo, prec + sbps)) : ~0ull;
-          uint64_t rk = min(key, dpp64_old<DPP_SHR1, 0xF>(key, ~0ull));
-          rk = min(rk, dpp64_old<DPP_SHR2, 0xF>(rk, ~0ull));
-          rk = min(rk, dpp64_old<DPP_SHR4, 0xF>(rk, ~0ull));
-          rk = min(rk, dpp64_old<DPP_SHR8, 0xF>(rk, ~0ull));
-          const uint64_t kmin = __shfl(rk, (lane & 48) | 15, 64);
-          const uint64_t bal = __ballot(on && key == kmin);
-          const uint32_t rowbits = (uint32_t)(bal >> (16 * gw)) & 0xFFFFu;
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // group leaders' lp rows -> all lanes
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-          __builtin_amdgcn_wave_barrier();
-          bool ok = false;
-          int o = 0, sh = 0;
-          int32_t q[MAXLAG];
-          if (nord > 0) {
-            o = (int)__builtin_ctz(rowbits);
-            double lpo[MAXLAG];
-#pragma unroll
-            for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[ws][o - 1][j];
-            ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
-          }
-          if (gon && lo == 0) {
-            const int m = 5 + gw;
-            S.mvalid[m] = ok ? 1 : 0;
-            S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
-#pragma unroll
-            for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
-          }
-        }
-      } else {
-        // levels 7-8 (up to 6 windows): Levinson-Durbin of window wi on wave wi % 4 in parallel
-      // 3.2 (fast 16-bit frames) the two FIXED candidates, searched on the two waves after the ones
-      // running Levinson-Durbin (psum is complete since the barrier above)
-      if (early) {
-        const int j = (wv - a.nwin % 4 + 4) % 4;  // this wave's slot after the LD waves
-        if (j < 2) {
-          int g1, g2;
-          fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
-          if (j == 0 && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
-          const int m = j == 0 ? g1 : g2;
-          if (m >= 0) {
-            const int pm = max_porder(n, m, cfg.max_porder);
-            uint64_t best = 0;
-            int bp = pm;
-            porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
-            if (lane == 0) {
-              S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
-              S.mporder[m] = bp;
-            }
+      // Levinson-Durbin, order choice and quantisation of 4 windows per wave at once: window wi on wave
+      // wi / 4, lanes 16 (wi % 4) .. +15 (the same op sequence per lane: one window's instruction cost for
+      // four) -> expected bits of order o on lane 16 (wi % 4) + o -> first minimum per lane group -> qlp
+      // quantisation per group.  Levels 3-6 (<= 3 windows) use wave 0, levels 7-8 (<= 6) waves 0-1; the
+      // two FIXED candidates are searched meanwhile on the next two waves (psum is complete since the
+      // autocorrelation barrier)
+      const int nldw = (a.nwin + 3) >> 2;
+      if (early && (wv == nldw || wv == nldw + 1)) {
+        int g1, g2;
+        fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
+        if (wv == nldw && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
+        const int m = wv == nldw ? g1 : g2;
+        if (m >= 0) {
+          const int pm = max_porder(n, m, cfg.max_porder);
+          uint64_t best = 0;
+          int bp = pm;
+          porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, S.kbest[m]);
+          if (lane == 0) {
+            S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
+            S.mporder[m] = bp;
           }
         }
       }
-      // 3.3 window wi on wave wi % 4, uniformly: autocorrelation -> Levinson-Durbin (registers) ->
-      // expected bits of every order in parallel (lane o) -> first minimum -> qlp quantisation
-      for (int wi = wv; wi < a.nwin; wi += 4) {
+      if (wv < nldw) {
+        const int gw = lane >> 4, lo = lane & 15;
+        const int wi = 4 * wv + gw;
+        const bool gon = wi < a.nwin;
+        const int ws = gon ? wi : 0;
         double ac[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++)
-          ac[l] = l <= lmax ? (S.red[wi][0][l] + S.red[wi][1][l]) + (S.red[wi][2][l] + S.red[wi][3][l])
-                                : 0.0;
-        const int m = 5 + wi;
+          ac[l] = l <= lmax ? (S.red[ws][0][l] + S.red[ws][1][l]) + (S.red[ws][2][l] + S.red[ws][3][l]) : 0.0;
         int nord = 0;
         double errv[MAXLAG];
-        if (ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[wv], errv, lane == 0);
+        if (gon && ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[ws], errv, lo == 0);
+        double e = errv[0];
+#pragma unroll
+        for (int j = 1; j < MAXLAG; j++)
+          if (lo == j + 1) e = errv[j];
+        // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as an
+        // unsigned integer; DPP min inside each 16-lane row (lane 15 of the row), lowest lane among
+        // the equal ones
+        const bool on = nord > 0 && lo >= 1 && lo <= nord;
+        const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lo, prec + sbps)) : ~0ull;
+        uint64_t rk = min(key, dpp64_old<DPP_SHR1, 0xF>(key, ~0ull));
+        rk = min(rk, dpp64_old<DPP_SHR2, 0xF>(rk, ~0ull));
+        rk = min(rk, dpp64_old<DPP_SHR4, 0xF>(rk, ~0ull));
+        rk = min(rk, dpp64_old<DPP_SHR8, 0xF>(rk, ~0ull));
+        const uint64_t kmin = __shfl(rk, (lane & 48) | 15, 64);
+        const uint64_t bal = __ballot(on && key == kmin);
+        const uint32_t rowbits = (uint32_t)(bal >> (16 * gw)) & 0xFFFFu;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // group leaders' lp rows -> all lanes
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
         bool ok = false;
         int o = 0, sh = 0;
         int32_t q[MAXLAG];
         if (nord > 0) {
-          double e = errv[0];
-#pragma unroll
-          for (int j = 1; j < MAXLAG; j++)
-            if (lane == j + 1) e = errv[j];
-          // first minimum over orders 1..nord: bits >= 0 and finite, so its IEEE pattern orders as
-          // an unsigned integer; DPP min over the wave, lowest lane among the equal ones
-          const bool on = lane >= 1 && lane <= nord;
-          const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lane, prec + sbps)) : ~0ull;
-          const uint64_t kmin = wave_min64(key);
-          o = (int)__builtin_ctzll(__ballot(on && key == kmin));
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's lp rows -> all lanes
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-          __builtin_amdgcn_wave_barrier();
+          o = (int)__builtin_ctz(rowbits);
           double lpo[MAXLAG];
 #pragma unroll
-          for (int j = 0; j < MAXLAG; j++) lpo[j] = S.lp[wv][o - 1][j];
+          for (int j = 0; j < MAXLAG; j++) lpo[j] = j < o ? S.lp[ws][lp_row(o - 1) + j] : 0.0;
           ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
         }
-        if (lane == 0) {
+        if (gon && lo == 0) {
+          const int m = 5 + wi;
           S.mvalid[m] = ok ? 1 : 0;
           S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
 #pragma unroll
           for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
         }
-          }
       }
     }
   }
@@ -688,6 +649,7 @@ read_x28(S.smp, t, x);
       for (int j = 0; j < 12 + kChunk; j++) xd[j] = (double)x[j];
 #pragma unroll
       for (int m = 0; m < 5; m++) {
+        if (fixfast) break;  // already summed by finite differences (phase 3a)
         constexpr double kF[5][4] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, -1, 0, 0}, {3, -3, 1, 0}, {4, -6, 4, -1}};
         const int skip = m > i0 ? m - i0 : 0;
         bool ovf = false;
@@ -773,7 +735,7 @@ read_x28(S.smp, t, x);
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp, B32 ? nullptr : S.kbest[B32 ? 0 : m]);
+    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp, S.kbest[m]);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
@@ -787,9 +749,9 @@ read_x28(S.smp, t, x);
   }
   __syncthreads();
   FRA_STOP(5)
-  if constexpr (!B32) {
+  {
     if (fastframe) {
-      // ---- 6+7, fast 16-bit frames: every wave derives the winner and the partition Rice parameters
+      // ---- 6+7, fast frames: every wave derives the winner and the partition Rice parameters
       // itself (same integers in every wave: no wave-0 section + broadcast barrier), exact sums by LDS
       // atomics, the same refinement in every wave, then the encoder.  4 barriers instead of 7.
       uint32_t key = ~0u;
@@ -803,11 +765,11 @@ read_x28(S.smp, t, x);
       const int pz = n >> ps;
       const bool live = i0 < n;
       const int pidx = live ? i0 / pz : 0;
-      const int k0 = S.kbest[B32 ? 0 : m][pidx];
+      const int k0 = S.kbest[m][pidx];
       // zig-zag residuals of the winner (exact code values), warm-up samples 0
       uint32_t uu[kChunk];
-read_x28(S.smp, t, x);
-      if (type == 2) {
+      read_x28(S.smp, t, x);
+      if (type == 2 && (!B32 || fixfast)) {  // FIXED: finite differences in 32 bits (range checked)
 #pragma unroll
         for (int k = 1; k <= 4; k++) {
           if (k <= o) {
@@ -821,17 +783,35 @@ read_x28(S.smp, t, x);
         int32_t q[MAXO];
 #pragma unroll
         for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
-        fra_short2 Q[(MAXO + 1) / 2];
-        q_pairs<(MAXO + 1) / 2>(q, Q);
+        if constexpr (B32) {  // exact predictor in f64 (|products| < 2^45, sums < 2^50); valid: fits int32
+          double qd[MAXO], xd2[12 + kChunk];
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj] - (pred_dot2<(MAXO + 1) / 2>(x, 12 + jj, Q) >> sh));
+          for (int j = 0; j < MAXO; j++) qd[j] = (double)q[j];
+#pragma unroll
+          for (int j = 0; j < 12 + kChunk; j++) xd2[j] = (double)x[j];
+          const double scale = ldexp(1.0, -sh);
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) {
+            double sum = 0.0;
+#pragma unroll
+            for (int j = 0; j < MAXO; j++) sum = fma(qd[j], xd2[11 + jj - j], sum);
+            uu[jj] = zz32((int32_t)(xd2[12 + jj] - floor(sum * scale)));
+          }
+        } else {
+          fra_short2 Q[(MAXO + 1) / 2];
+          q_pairs<(MAXO + 1) / 2>(q, Q);
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj] - (pred_dot2<(MAXO + 1) / 2>(x, 12 + jj, Q) >> sh));
+        }
       }
       if (head) {
 #pragma unroll
         for (int jj = 0; jj < 12; jj++)
           if (jj < o) uu[jj] = 0u;
       }
-      uint32_t fs0 = 0, fs1 = 0, fs2 = 0;  // u < 2^28: 16 of them fit 32 bits
+      if (B32 && t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the next barrier
+      // 16-bit: u < 2^28, so 16 of them fit 32 bits; 32-bps: 64-bit partial sums
+      typename std::conditional<B32, uint64_t, uint32_t>::type fs0 = 0, fs1 = 0, fs2 = 0;
       {
         const int km = k0 > 0 ? k0 - 1 : 0;  // fs0 is only used when k0 >= 1
 #pragma unroll
@@ -878,7 +858,7 @@ read_x28(S.smp, t, x);
       FRA_STOP(6)
       // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
       const int npp = 1 << ps;
-      const int k0j = lane < npp ? (int)S.kbest[B32 ? 0 : m][lane] : 0;
+      const int k0j = lane < npp ? (int)S.kbest[m][lane] : 0;
       uint64_t best = 0;
       int bk = 0;
       if (lane < npp) {
@@ -915,7 +895,12 @@ read_x28(S.smp, t, x);
       // encode (RFC 9639 9.2) into the LDS bit buffer (over psum: every wave is past its psum reads)
       const uint32_t fbits = verbatim ? verb : (uint32_t)exact;
       const uint32_t nw = (fbits + 31) >> 5;
-      uint32_t* buf = S.u.buf;
+      if (B32 && verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
+        verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+        return;
+      }
+      // 32-bps: the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
+      uint32_t* buf = B32 ? reinterpret_cast<uint32_t*>(S.smp) : S.u.buf;
       for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
       const int pb = big ? 5 : 4;
       const int dk = kcur - k0;
@@ -937,7 +922,8 @@ read_x28(S.smp, t, x);
       if (verbatim) {
         for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
       } else {
-        if (t < o) lds_put(buf, hdr + (uint32_t)t * sbps, (uint32_t)S.smp[sidx(t)] & smask, sbps);
+        if (t < o)
+          lds_put(buf, hdr + (uint32_t)t * sbps, (uint32_t)(B32 ? S.warm[t] : (int32_t)S.smp[sidx(t)]) & smask, sbps);
         uint32_t pos = hdr + (uint32_t)o * sbps;
         if (type == 3) {
           if (t == 0) {
@@ -1157,22 +1143,8 @@ read_x28(S.smp, t, x);
   const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
   if constexpr (B32) {
     if (ftype == 1) {
-      // VERBATIM (rare): each output word assembled from the <= 3 samples it covers, straight from smp
-      // to the slot (smp is still intact: the aliased bit buffer is not touched on this path)
-      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
-      const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
-      for (uint32_t j = t; j < nw; j += kThreads) {
-        const int64_t wb = 32 * (int64_t)j;
-        uint32_t word = j == 0 ? (uint32_t)(hv >> 32) : (j == 1 ? (uint32_t)hv : 0u);
-        int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
-        for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
-          const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
-          const int sft = 32 - (int)rel - sbps;
-          const uint64_t v = (uint64_t)((uint32_t)S.smp[sidx(s)] & smask);
-          word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
-        }
-        slot[j] = word;
-      }
+      // VERBATIM (rare): straight from smp to the slot (the aliased bit buffer is not touched)
+      verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
       return;
     }
   }

@@ -485,8 +485,10 @@ __device__ inline int best_order_by_error(const double* err, int norders, int n,
 // Levinson-Durbin run uniformly by a whole wave from register-resident autocorrelation: errors
 // stay in registers (errv), coefficient rows go to LDS from lane 0 only.  Same op sequence as
 // oracle ora_levinson.
+// LD coefficient rows, row i (order i + 1, i + 1 entries) at lp[i (i + 1) / 2 ...] (triangular)
+__host__ __device__ constexpr int lp_row(int i) { return i * (i + 1) / 2; }
 template <int MAXLAG>
-__device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_order, double (*lp)[MAXLAG],
+__device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_order, double* lp,
                                     double (&errv)[MAXLAG], bool writer) {
   double lpc[MAXLAG];
 #pragma unroll
@@ -512,7 +514,7 @@ __device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_orde
       err = err * (1.0 - r * r);
       if (writer) {
 #pragma unroll
-        for (int j = 0; j <= i; j++) lp[i][j] = -lpc[j];
+        for (int j = 0; j <= i; j++) lp[lp_row(i) + j] = -lpc[j];
       }
       errv[i] = err;
       if (!(err > 0.0)) {
