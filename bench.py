@@ -419,6 +419,13 @@ def main():
             size_c2 = round(len(fr) / 178857.0, 5)
         except Exception:
             size_c2 = None
+        # pyflac-shim latency per stream on C2 (sample_rgb, 65,536 x 3 int16 samples; the reference's
+        # per-tile call shape: StreamEncoder(...).process(audio); finish())
+        shim = None
+        try:
+            shim = measure_shim_c2(N)
+        except Exception as e:  # reported, never fatal for the headline line
+            shim = {"error": f"{type(e).__name__}: {e}"}
         # counters of the dominant kernel: in-run passes (this build), else the committed file if current.
         # The passes run in a child process: release this process's device buffers first.
         plan.close()
@@ -477,6 +484,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_mp": cpu_mp,
             "size_ratio_vs_libflac_c2": size_c2,
+            "pyflac_shim_c2": shim,
             "e2e": e2e,
         }
         print(json.dumps(result), flush=True)
@@ -486,6 +494,34 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def measure_shim_c2(N):
+    from flac_raster.encoder import StreamEncoder
+    from flac_raster.normalization import normalize_to_audio
+    from flac_raster.tiff import read_geotiff
+
+    rgb, _ = read_geotiff(ROOT / "tests" / "golden" / "sample_rgb.tif")
+    audio, _ = normalize_to_audio(rgb.transpose(1, 2, 0).reshape(-1, 3), 16)
+    out = []
+
+    def one(enc):
+        enc.process(audio)
+        enc.finish()
+
+    N.release_pinned_pool()
+    t0 = time.perf_counter()
+    one(StreamEncoder(44100, lambda b, n, s, f: out.append(n), compression_level=5, blocksize=4096))  # cold
+    t_cold = time.perf_counter() - t0
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one(StreamEncoder(44100, lambda b, n, s, f: out.append(n), compression_level=5, blocksize=4096))
+    t_new = (time.perf_counter() - t0) / reps
+    return {"ms_first_stream": round(t_cold * 1e3, 3), "ms_per_stream": round(t_new * 1e3, 3),
+            "what": "StreamEncoder(...).process(65,536 x 3 int16) + finish() incl. 19 write callbacks, a new encoder "
+                    "per stream (the reference's per-tile shape); the first stream builds the GPU plan, later "
+                    "ones of the same shape take it from the process-wide plan pool"}
 
 
 def measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, dev_plan):

@@ -375,6 +375,7 @@ static int plan_build(fra_plan* p) {
     st.nsamples = (int64_t)wd.width * wd.height;
     st.sample_rate = j.sample_rate > 0 ? j.sample_rate : sample_rate_for_pixels(st.nsamples);
     st.first_frame = (int32_t)nf_total;
+    st.frame_number0 = (uint32_t)j.first_frame;
     const int64_t nfr = (st.nsamples + j.blocksize - 1) / j.blocksize;
     st.nframes = (int32_t)nfr;
     if (st.nsamples > 0) {
@@ -592,6 +593,7 @@ int fra_plan_create(fra_ctx* ctx, const fra_job* job, fra_plan** out) {
   if (job->norm == 0 && job->dtype != FRA_I16 && job->dtype != FRA_I32)
     return set_err(FRA_E_INVALID, "norm == 0 (pre-normalised audio) needs int16 or int32 samples");
   if (job->nwindows < 0 || (job->nwindows > 0 && !job->windows)) return set_err(FRA_E_INVALID, "bad windows");
+  if (job->first_frame < 0) return set_err(FRA_E_INVALID, "first_frame must be >= 0");
   for (int w = 0; w < job->nwindows; w++) {
     const fra_window& wd = job->windows[w];
     if (wd.height < 0 || wd.width < 0 || wd.row_off < 0 || wd.col_off < 0 || (wd.height > 0) != (wd.width > 0))
@@ -786,6 +788,18 @@ int fra_plan_timing(fra_plan* p, float* ms4, int32_t* n) {
   collect_times(p);
   for (int k = 0; k < 4; k++) ms4[k] = p->ms[k];
   *n = p->nexec;
+  return FRA_OK;
+}
+
+int fra_plan_set_first_frame(fra_plan* p, int32_t first_frame) {
+  if (!p || first_frame < 0) return set_err(FRA_E_INVALID, "bad argument");
+  (void)hipSetDevice(p->ctx->device);
+  p->job.first_frame = first_frame;
+  for (auto& st : p->streams) st.frame_number0 = (uint32_t)first_frame;
+  if (!p->streams.empty())  // ordered before the next execute on the plan's stream
+    HIPCHK(hipMemcpyAsync(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(),
+                          hipMemcpyHostToDevice, p->ctx->stream));
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));  // the host array may change again before it is read
   return FRA_OK;
 }
 

@@ -751,7 +751,7 @@ __device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameD
   h[p++] = 0xF8;
   h[p++] = (uint8_t)((bc << 4) | sc);
   h[p++] = (uint8_t)(((st.channels - 1) << 4) | (bps_code(st.bps) << 1));
-  const uint32_t v = (uint32_t)fr.index;
+  const uint32_t v = (uint32_t)fr.index + st.frame_number0;
   const int nb = utf8_len(v);
   if (nb == 1) h[p++] = (uint8_t)v;
   else {
@@ -768,7 +768,7 @@ __device__ inline int frame_header_len(const StreamDev& st, const FrameDev& fr) 
   int bsx, srx, srv;
   bs_code(fr.n, &bsx);
   sr_code(st.sample_rate, &srx, &srv);
-  return 4 + utf8_len((uint32_t)fr.index) + bsx / 8 + srx / 8 + 1;  // + CRC-8
+  return 4 + utf8_len((uint32_t)fr.index + st.frame_number0) + bsx / 8 + srx / 8 + 1;  // + CRC-8
 }
 
 }  // namespace fra

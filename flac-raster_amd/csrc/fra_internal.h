@@ -135,6 +135,8 @@ struct StreamDev {
   int32_t sample_rate;
   int32_t first_frame, nframes;
   int64_t nsamples;      // per channel (= width*height)
+  uint32_t frame_number0;  // FLAC frame number of the stream's first frame (pyflac shim: blocks already emitted)
+  uint32_t pad_;
 };
 
 struct FrameDev {

@@ -48,7 +48,7 @@ class Job(C.Structure):
         ("raster", C.c_void_p), ("raster_on_device", C.c_int32), ("dtype", C.c_int32), ("channels", C.c_int32),
         ("band_stride", C.c_int64), ("row_stride", C.c_int64), ("col_stride", C.c_int64),
         ("windows", C.POINTER(Window)), ("nwindows", C.c_int32), ("level", C.c_int32), ("blocksize", C.c_int32),
-        ("norm", C.c_int32), ("sample_rate", C.c_int32),
+        ("norm", C.c_int32), ("sample_rate", C.c_int32), ("first_frame", C.c_int32),
     ]
 
 
@@ -89,7 +89,7 @@ EXPORTS = [
     "fra_plan_destroy", "fra_encode", "fra_stream_header", "fra_synth_raster", "fra_device_alloc",
     "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d", "fra_plan_frame_offsets", "fra_normalize",
     "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
-    "fra_host_register", "fra_host_unregister", "fra_tiff_decode",
+    "fra_host_register", "fra_host_unregister", "fra_tiff_decode", "fra_plan_set_first_frame",
 ]
 
 
@@ -138,6 +138,7 @@ def load():
         L.fra_decode.argtypes = [vp, u64, i32, C.POINTER(Decoded), C.POINTER(C.POINTER(C.c_int32))]
         L.fra_plan_encode_host.argtypes = [vp, vp, vp, u64, C.POINTER(u64)]
         L.fra_plan_capacity.argtypes = [vp, C.POINTER(u64), C.POINTER(i32)]
+        L.fra_plan_set_first_frame.argtypes = [vp, i32]
         L.fra_host_alloc.argtypes = [u64, C.POINTER(vp)]
         L.fra_host_free.argtypes = [vp]
         L.fra_host_register.argtypes = [vp, u64]
@@ -357,6 +358,10 @@ class Plan:
         _check(load().fra_plan_download(self.h, buf.ctypes.data_as(C.c_void_p), total))
         return infos, buf[:total].tobytes()
 
+    def set_first_frame(self, n: int):
+        """FLAC frame number of every stream's first frame for the next execute (pyflac shim)."""
+        _check(load().fra_plan_set_first_frame(self.h, int(n)))
+
     def capacity(self) -> Tuple[int, int]:
         """(upper bound of the output bytes, number of host-pipeline row bands)."""
         cap, nb = C.c_uint64(), C.c_int32()
@@ -411,6 +416,37 @@ class Plan:
 
 
 _default_ctx = {}
+
+# Process-wide pool of idle plans keyed by job shape: the reference creates one encoder per tile
+# (spatial_encoder.py:291-304), and tiles of one raster share a few shapes, so a released plan (with its
+# page-locked output buffer) is handed to the next encoder of the same shape instead of rebuilding the
+# device workspace (~20 ms of allocations and table uploads).  Plans are used by one owner at a time.
+_PLAN_POOL_MAX = int(os.environ.get("FRA_PLAN_POOL", "16"))
+_plan_pool: "dict" = {}
+_plan_pool_n = 0
+
+
+def acquire_plan(key, factory):
+    """An idle pooled plan entry for ``key`` or a new one from ``factory()``; the caller owns it until
+    :func:`release_plan`."""
+    global _plan_pool_n
+    with _lock:
+        lst = _plan_pool.get(key)
+        if lst:
+            _plan_pool_n -= 1
+            return lst.pop()
+    return factory()
+
+
+def release_plan(key, entry):
+    """Return a plan entry ``(plan, ...)`` to the pool (closed instead when the pool is full)."""
+    global _plan_pool_n
+    with _lock:
+        if _plan_pool_n < _PLAN_POOL_MAX:
+            _plan_pool.setdefault(key, []).append(entry)
+            _plan_pool_n += 1
+            return
+    entry[0].close()
 
 
 def default_context(device: int = 0) -> Context:

@@ -12,21 +12,27 @@ Drop-in for the two reference call sites::
 ``docs/sonos-pyflac.txt:1968-2014, 2175-2212, 2311-2332``):
 
 * the first ``process()`` fixes ``channels = samples.shape[1]`` and
-  ``bits_per_sample = samples.dtype.itemsize * 8`` (int16 -> 16-bps, int32 -> 32-bps FLAC);
+  ``bits_per_sample = samples.dtype.itemsize * 8`` (int16 -> 16-bps, int32 -> 32-bps FLAC) and
+  initialises the stream: the write callback receives ``fLaC`` (4 B), the STREAMINFO block (38 B) and
+  the VORBIS_COMMENT block (44 B) with ``num_samples = 0`` right there, as libFLAC's ``init_stream``
+  does under pyflac's ``_init`` (``:1986-1991``, ``:2200-2212``);
 * ``blocksize=0`` takes the level's default (1152 for levels 0-2, 4096 for 3-8);
-* the write callback receives, in order, ``fLaC`` (4 B), the STREAMINFO block (38 B) and the
-  VORBIS_COMMENT block (44 B) with ``num_samples = 0``, then one call per frame with
-  ``num_samples = blocksize of that frame`` and ``current_frame = frame number``
-  (libFLAC 1.4.3 stream encoder, ``:6601-6637``);
-* encoding happens on the GPU at ``finish()`` (libFLAC emits full blocks during ``process``; the
-  bytes and the callback sequence are the same, only the timing of the calls differs).
+* every ``process()`` encodes, on the GPU, the complete blocks it can and calls back once per frame
+  (``num_samples`` = the frame's block size, ``current_frame`` = its number).  Like libFLAC 1.4.3's
+  ``process_interleaved`` (stream_encoder.c keeps one sample of look-ahead, ``OVERREAD_``: a block is
+  encoded once blocksize + 1 samples are buffered, the final block only by ``finish()``), the samples
+  of the last block stay buffered until more arrive or ``finish()`` flushes them.  libFLAC's source is
+  not in this container; that timing rule is restated from the public libFLAC sources and is not
+  pinned by a fixture here.  Bytes are independent of how the samples are split across calls.
+* GPU plans are cached per block count, so repeated calls of one size reuse their device workspace.
 """
 
 from __future__ import annotations
 
 import enum
 import logging
-from typing import Callable, List, Optional
+from collections import OrderedDict
+from typing import Callable, Optional
 
 import numpy as np
 
@@ -68,6 +74,8 @@ def default_blocksize(level: int) -> int:
 class StreamEncoder:
     """GPU FLAC stream encoder with pyflac's constructor, ``process``/``finish`` and callbacks."""
 
+    _PLAN_CACHE = 4
+
     def __init__(self, sample_rate: int, write_callback: Callable[[bytes, int, int, int], None],
                  seek_callback: Callable = None, tell_callback: Callable = None, metadata_callback: Callable = None,
                  compression_level: int = 5, blocksize: int = 0, streamable_subset: bool = True,
@@ -86,7 +94,9 @@ class StreamEncoder:
         self._channels = None
         self._bits_per_sample = None
         self._initialised = False
-        self._chunks: List[np.ndarray] = []
+        self._pending: Optional[np.ndarray] = None
+        self._next_frame = 0
+        self._plans: "OrderedDict" = OrderedDict()  # block count -> (plan, page-locked output buffer)
         self._state = EncoderState.UNINITIALIZED
         self.logger = logging.getLogger("flac_raster.encoder")
 
@@ -109,8 +119,16 @@ class StreamEncoder:
         if not 0 < self._sample_rate < (1 << 20):
             raise EncoderInitException("INVALID_SAMPLE_RATE", f"sample rate {self._sample_rate}")
         self._bs = bs
+        self._dtype = np.int16 if self._bits_per_sample == 16 else np.int32
+        self._pending = np.empty((0, self._channels), self._dtype)
+        self._next_frame = 0
         self._initialised = True
         self._state = EncoderState.OK
+        # libFLAC init_stream: the stream header reaches the write callback during initialisation
+        header = _native.stream_header(self._channels, self._bits_per_sample, self._sample_rate, self._bs)
+        self._emit(header[:4], 0, 0)
+        self._emit(header[4:42], 0, 0)
+        self._emit(header[42:86], 0, 0)
 
     def process(self, samples: np.ndarray):
         if not isinstance(samples, np.ndarray):
@@ -123,32 +141,78 @@ class StreamEncoder:
         if s.shape[1] != self._channels:
             self._state = EncoderState.CLIENT_ERROR
             raise EncoderProcessException(str(self._state))
-        dt = np.int16 if self._bits_per_sample == 16 else np.int32
-        self._chunks.append(np.ascontiguousarray(s).astype(dt, copy=True))
+        s = np.ascontiguousarray(s).astype(self._dtype, copy=False)
+        pend = np.concatenate([self._pending, s]) if len(self._pending) else np.ascontiguousarray(s)
+        nblk = (len(pend) - 1) // self._bs if len(pend) > self._bs else 0  # one sample of look-ahead
+        if nblk:
+            self._encode_emit(pend[: nblk * self._bs])
+            pend = pend[nblk * self._bs:]
+        self._pending = pend.copy() if pend.base is not None else pend
 
     def finish(self) -> bool:
         if not self._initialised:
             return True
-        samples = (np.concatenate(self._chunks) if len(self._chunks) != 1 else self._chunks[0])
-        self._chunks = []
-        try:
-            info, frames, offsets = _native.encode_interleaved(samples, self._sample_rate, self._compression_level,
-                                                               self._bs, self._device, return_offsets=True)
-        except _native.NativeError as e:
-            self._state = EncoderState.MEMORY_ALLOCATION_ERROR
-            raise EncoderProcessException(str(e)) from e
-        header = _native.stream_header(self._channels, self._bits_per_sample, self._sample_rate, self._bs)
-        self._emit(header[:4], 0, 0)
-        self._emit(header[4:42], 0, 0)
-        self._emit(header[42:86], 0, 0)
-        n = len(samples)
-        mv = memoryview(frames)
-        for i in range(len(offsets) - 1):
-            a, b = int(offsets[i]), int(offsets[i + 1])
-            self._emit(bytes(mv[a:b]), min(self._bs, n - i * self._bs), i)
+        if len(self._pending):
+            self._encode_emit(self._pending)
+        self._pending = None
+        self.close()
         self._initialised = False
         self._state = EncoderState.UNINITIALIZED
         return True
+
+    def _plan_key(self, n: int):
+        return ("shim", self._device, np.dtype(self._dtype).str, self._channels, n, self._compression_level,
+                self._bs, self._sample_rate)
+
+    def _plan_for(self, n: int):
+        if n in self._plans:
+            self._plans.move_to_end(n)
+            return self._plans[n]
+
+        def make():
+            ctx = _native.default_context(self._device)
+            C = self._channels
+            plan = _native.Plan(ctx, None, False, self._dtype, C, (1, n * C, C), [(0, 0, 1, n)],
+                                self._compression_level, self._bs, 0, self._sample_rate)
+            cap, _ = plan.capacity()
+            return (plan, _native.pinned_empty(cap, np.uint8))
+
+        ent = _native.acquire_plan(self._plan_key(n), make)
+        self._plans[n] = ent
+        while len(self._plans) > self._PLAN_CACHE:
+            k, old = self._plans.popitem(last=False)
+            _native.release_plan(self._plan_key(k), old)
+        return ent
+
+    def _encode_emit(self, block: np.ndarray):
+        n = len(block)
+        try:
+            plan, out = self._plan_for(n)
+            plan.set_first_frame(self._next_frame)
+            plan.encode_host(block, out)
+            nfr = (n + self._bs - 1) // self._bs
+            offsets = plan.frame_offsets(nfr)
+        except _native.NativeError as e:
+            self._state = EncoderState.MEMORY_ALLOCATION_ERROR
+            raise EncoderProcessException(str(e)) from e
+        mv = memoryview(out)
+        for i in range(nfr):
+            a, b = int(offsets[i]), int(offsets[i + 1])
+            self._emit(bytes(mv[a:b]), min(self._bs, n - i * self._bs), self._next_frame + i)
+        self._next_frame += nfr
+
+    def close(self):
+        """Hand this encoder's GPU plans back to the process-wide pool (the next encoder of the same
+        shape reuses them).  Also done by ``finish()`` and on garbage collection."""
+        for k, ent in self._plans.items():
+            _native.release_plan(self._plan_key(k), ent)
+        self._plans.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _emit(self, buf: bytes, num_samples: int, current_frame: int):
         try:

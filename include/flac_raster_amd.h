@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define FRA_ABI_VERSION 2
+#define FRA_ABI_VERSION 3
 
 #if defined(__GNUC__) || defined(__clang__)
 #define FRA_API __attribute__((visibility("default")))
@@ -81,6 +81,8 @@ typedef struct {
   int32_t blocksize;        /* samples per frame, 16..4096 (reference passes 4096) */
   int32_t norm;             /* 0: samples already audio ints (pyflac path); 16 / 24: normalize_to_audio */
   int32_t sample_rate;      /* 0: calculate_audio_params rule from window H*W (normalization.py:108-120) */
+  int32_t first_frame;      /* FLAC frame number of every stream's first frame (0; the pyflac shim
+                               continues a stream across process() calls, sonos-pyflac.txt:1968-2001) */
 } fra_job;
 
 typedef struct {
@@ -134,6 +136,8 @@ FRA_API void fra_plan_destroy(fra_plan *plan);
  * host_out.  A plan's capacity bound: fra_plan_capacity. */
 FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
                                  uint64_t *total_bytes);
+/* frame number of every stream's first frame for the next execute (the job's first_frame until set) */
+FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
 FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
 

@@ -90,6 +90,8 @@ def test_stream_encoder_callback_sequence(golden_dir):
                         compression_level=5, blocksize=4096)
     enc._channels, enc._bits_per_sample = 3, 16  # what the reference sets; overridden by process (F3)
     enc.process(audio)
+    # header at init (first process), then every block but the last (libFLAC keeps one sample of look-ahead)
+    assert len(calls) == 3 + 15 and [c[1] for c in calls[:3]] == [4, 38, 44]
     assert enc.finish()
     ref, fb, _ = O.encode(audio, 44100, level=5, return_info=True)
     assert [c[1] for c in calls[:3]] == [4, 38, 44] and calls[0][0] == b"fLaC"
@@ -98,6 +100,32 @@ def test_stream_encoder_callback_sequence(golden_dir):
     assert [c[1] for c in fr] == list(fb) and [c[3] for c in fr] == list(range(16))
     assert all(c[2] == 4096 for c in fr) and all(len(c[0]) == c[1] for c in calls)
     assert b"".join(c[0] for c in calls) == ref
+
+
+def test_stream_encoder_incremental_emission(golden_dir):
+    """pyflac/libFLAC call timing: frames are emitted during process() as soon as blocksize + 1 samples
+    are buffered, numbered continuously across calls; the tail waits for finish()."""
+    audio = _rgb_audio(golden_dir)
+    calls = []
+    enc = StreamEncoder(44100, lambda b, n, s, f: calls.append((bytes(b), s, f)), compression_level=5, blocksize=4096)
+    fed = 0
+    for part in np.array_split(audio, 13):  # 5041-5042 samples per call
+        enc.process(part)
+        fed += len(part)
+        assert len(calls) == 3 + max(0, (fed - 1) // 4096)
+    assert enc.finish()
+    assert [c[2] for c in calls[3:]] == list(range(16)) and all(c[1] == 4096 for c in calls[3:])
+    assert b"".join(c[0] for c in calls) == O.encode(audio, 44100, level=5)
+    # exact multiples and single-sample calls
+    calls.clear()
+    enc = StreamEncoder(44100, lambda b, n, s, f: calls.append((bytes(b), s, f)), compression_level=5, blocksize=4096)
+    enc.process(audio[:4096])
+    assert len(calls) == 3
+    enc.process(audio[4096:4097])
+    assert len(calls) == 4 and calls[3][2] == 0
+    enc.process(audio[4097:])
+    enc.finish()
+    assert b"".join(c[0] for c in calls) == O.encode(audio, 44100, level=5)
 
 
 def test_stream_encoder_multi_process_and_defaults(golden_dir):

@@ -48,7 +48,7 @@ def test_abi_exports_every_declared_symbol():
     missing = [s for s in sorted(decl) if not hasattr(L, s)]
     assert not missing, missing
     assert set(N.EXPORTS) == decl
-    assert L.fra_abi_version() == 2
+    assert L.fra_abi_version() == 3
 
 
 def test_abi_errors_without_device():
