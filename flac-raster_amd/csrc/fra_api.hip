@@ -119,6 +119,19 @@ struct fra_plan {
   hipEvent_t hev_start = nullptr;
   unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
   unsigned long long* d_gbase_mirror = nullptr;  // its device address
+  // cross-execute pipelining (FRA_PIPE, default on when a second buffer set fits in a third of the free
+  // device memory, single frame group): execute k analyses into buffer set k % 2 on the plan's stream
+  // while k_assemble of execute k-1 (reading the other set) runs on the pack stream
+  bool pipe = false;
+  int cur = 0;  // buffer set of the last execute
+  SfDesc* sf2[2] = {};
+  uint32_t* tmp2[2] = {};
+  uint32_t* fmeta2[2] = {};
+  unsigned long long* fbytes2[2] = {};
+  unsigned long long* foff2[2] = {};
+  hipStream_t pack = nullptr;
+  hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
+  bool pack_pending[2] = {false, false};
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -265,6 +278,21 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_win);
   (void)hipFree(p->d_wrange);
+  if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
+    for (int b = 0; b < 2; b++) {
+      (void)hipFree(p->sf2[b]);
+      (void)hipFree(p->fbytes2[b]);
+      (void)hipFree(p->foff2[b]);
+      (void)hipFree(p->tmp2[b]);
+      (void)hipFree(p->fmeta2[b]);
+    }
+    p->d_sf = nullptr; p->d_fbytes = nullptr; p->d_foff = nullptr; p->d_tmp = nullptr; p->d_fmeta = nullptr;
+  }
+  if (p->pack) (void)hipStreamDestroy(p->pack);
+  for (int b = 0; b < 2; b++) {
+    if (p->ev_scan[b]) (void)hipEventDestroy(p->ev_scan[b]);
+    if (p->ev_pack[b]) (void)hipEventDestroy(p->ev_pack[b]);
+  }
   (void)hipFree(p->d_sf);
   (void)hipFree(p->d_fbytes);
   (void)hipFree(p->d_foff);
@@ -562,6 +590,58 @@ static int plan_build(fra_plan* p) {
   a.level = j.level;
   a.nwin = std::max(1, p->nwin);
   for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
+  {  // second buffer set for cross-execute pipelining
+    const char* ev = getenv("FRA_PIPE");
+    // large plans only: small ones (the pyflac shim, single tiles) execute once per plan, and the
+    // measured gain is the tail of k_analyze (k_assemble cannot co-reside with it: 6 analysis workgroups
+    // leave 32 VGPRs and 7.9 KiB of LDS per CU/SIMD) -- C3 1.610 -> 1.586 ms, C4 2.422 -> 2.408 ms
+    const bool want = !(ev && atoi(ev) == 0) && p->groups.size() == 1 && nfr >= 4096;
+    const size_t nsf = (size_t)nfr * p->cmax;
+    const size_t extra = sizeof(SfDesc) * nsf + sizeof(uint32_t) * (size_t)p->tmp_stride * nsf +
+                         sizeof(uint32_t) * kMetaWords * nfr + 2 * sizeof(unsigned long long) * (nfr + 1);
+    size_t freeb = 0, totalb = 0;
+    if (want && hipMemGetInfo(&freeb, &totalb) == hipSuccess && extra <= freeb / 3) {
+      p->sf2[0] = p->d_sf; p->tmp2[0] = p->d_tmp; p->fmeta2[0] = p->d_fmeta;
+      p->fbytes2[0] = p->d_fbytes; p->foff2[0] = p->d_foff;
+      p->pipe = true;  // from here on destroy frees through the arrays
+      HIPCHK(hipMalloc(&p->sf2[1], sizeof(SfDesc) * std::max<size_t>(1, nsf)));
+      HIPCHK(hipMalloc(&p->tmp2[1], sizeof(uint32_t) * (size_t)p->tmp_stride * std::max<size_t>(1, nsf)));
+      HIPCHK(hipMalloc(&p->fmeta2[1], sizeof(uint32_t) * kMetaWords * nfr));
+      HIPCHK(hipMalloc(&p->fbytes2[1], sizeof(unsigned long long) * (nfr + 1)));
+      HIPCHK(hipMalloc(&p->foff2[1], sizeof(unsigned long long) * (nfr + 1)));
+      HIPCHK(hipStreamCreateWithFlags(&p->pack, hipStreamNonBlocking));
+      for (int b = 0; b < 2; b++) {
+        HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_pack[b], hipEventDisableTiming));
+      }
+    }
+  }
+  return FRA_OK;
+}
+
+// point the plan (and its kernel arguments) at buffer set b
+static void use_buffers(fra_plan* p, int b) {
+  if (!p->pipe) return;
+  p->d_sf = p->sf2[b]; p->d_tmp = p->tmp2[b]; p->d_fmeta = p->fmeta2[b];
+  p->d_fbytes = p->fbytes2[b]; p->d_foff = p->foff2[b];
+  p->args.sf = p->d_sf; p->args.tmp = p->d_tmp; p->args.fmeta = p->d_fmeta;
+  p->args.frame_bytes = p->d_fbytes; p->args.frame_off = p->d_foff;
+  p->cur = b;
+}
+// make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
+static int drain_pipeline(fra_plan* p) {
+  if (!p->pipe) return FRA_OK;
+  for (int b = 0; b < 2; b++)
+    if (p->pack_pending[b]) {
+      HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_pack[b], 0));
+      p->pack_pending[b] = false;
+    }
+  use_buffers(p, 0);
+  return FRA_OK;
+}
+static int plan_sync_all(fra_plan* p) {
+  if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));
   return FRA_OK;
 }
 
@@ -632,7 +712,8 @@ static void collect_times(fra_plan* p) {
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
 static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
                      hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan, int slot = -1,
-                     unsigned long long* host_mirror = nullptr) {
+                     unsigned long long* host_mirror = nullptr, hipStream_t pack_st = nullptr,
+                     hipEvent_t ev_scan = nullptr) {
   const JobArgs& a = p->args;
   const int nst = gr.w1 - gr.w0, nf = gr.f1 - gr.f0;
   // the minmax family indexes streams by blockIdx.y: launched per chunk of <= kMaxGridY windows, with the
@@ -666,7 +747,13 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
                               a.nframes_total, st, host_mirror));
   if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
   if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
-  HIPCHK(launch_assemble(ga, st));
+  if (pack_st) {  // assembly on the pack stream once this group's offsets exist
+    HIPCHK(hipEventRecord(ev_scan, st));
+    HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
+    HIPCHK(launch_assemble(ga, pack_st));
+  } else {
+    HIPCHK(launch_assemble(ga, st));
+  }
   return FRA_OK;
 }
 
@@ -678,6 +765,20 @@ int fra_plan_execute(fra_plan* p) {
   if (p->timing) collect_times(p);
   p->args.vec8 = (p->ld_vec8 && (uintptr_t)p->d_raster % 8 == 0) ? 1 : 0;
   int rc = FRA_OK;
+  if (p->pipe && !p->timing) {
+    // cross-execute pipelining: this execute's analysis overlaps the previous execute's k_assemble
+    const int b = p->cur ^ 1;
+    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(s, p->ev_pack[b], 0));  // execute k-2 is done with set b
+    use_buffers(p, b);
+    rc = run_group(p, p->groups[0], 0, 1, s, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
+                   p->ev_scan[b]);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(p->ev_pack[b], p->pack));
+    p->pack_pending[b] = true;
+    p->executed = true;
+    return FRA_OK;
+  }
+  if ((rc = drain_pipeline(p))) return rc;
   if (p->timing || p->groups.size() == 1) {
     // serial: the whole plan as one group; timing events bracket each kernel phase
     if (p->timing) HIPCHK(hipEventRecord(p->ev[0], s));
@@ -709,7 +810,7 @@ int fra_plan_execute(fra_plan* p) {
 int fra_plan_sync(fra_plan* p) {
   if (!p) return set_err(FRA_E_INVALID, "null plan");
   (void)hipSetDevice(p->ctx->device);
-  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  if (int rc = plan_sync_all(p)) return rc;
   if (p->timing) collect_times(p);
   return FRA_OK;
 }
@@ -718,7 +819,7 @@ int fra_plan_result(fra_plan* p, fra_stream_info* infos, uint64_t* total) {
   if (!p) return set_err(FRA_E_INVALID, "null plan");
   if (!p->executed) return set_err(FRA_E_STATE, "plan not executed");
   (void)hipSetDevice(p->ctx->device);
-  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  if (int rc = plan_sync_all(p)) return rc;
   const int nfr = p->args.nframes_total;
   std::vector<unsigned long long> off(nfr + 1);
   HIPCHK(hipMemcpy(off.data(), p->d_foff, sizeof(unsigned long long) * (nfr + 1), hipMemcpyDeviceToHost));
@@ -761,7 +862,7 @@ int fra_plan_frame_offsets(fra_plan* p, uint64_t* offsets, uint64_t n) {
   if (n != nfr + 1) return set_err(FRA_E_INVALID, "frame offsets: n = %llu, plan has %llu frames + 1",
                                    (unsigned long long)n, (unsigned long long)nfr);
   (void)hipSetDevice(p->ctx->device);
-  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  if (int rc = plan_sync_all(p)) return rc;
   static_assert(sizeof(unsigned long long) == sizeof(uint64_t), "u64");
   HIPCHK(hipMemcpy(offsets, p->d_foff, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
   return FRA_OK;
@@ -840,6 +941,7 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
     p->executed = true;
     return FRA_OK;
   }
+  if (int rc = drain_pipeline(p)) return rc;  // the bands below use buffer set 0 on the plan's stream
   if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
   p->d_raster = p->d_raster_owned;
   p->args.raster = p->d_raster;
