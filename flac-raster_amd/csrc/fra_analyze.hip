@@ -358,12 +358,16 @@ template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  const int g = a.frame_base + (int)blockIdx.x, c = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = a.frame_base + (int)blockIdx.x, c = a.c_base + (int)blockIdx.y, t = threadIdx.x, lane = t & 63,
+            wv = t >> 6;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
-  if (c >= st.channels) return;
+  // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; M and S (bps + 1 bits) are
+  // analysed by the 32-bit instance (launched with c_base 2), L and R by the 16-bit one
+  if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
   const int n = fr.n;
-  const int bps = st.bps;
+  const int bps = st.bps + ((st.ms && c == 3) ? 1 : 0);
+  const int msmode = (st.ms && c >= 2) ? c - 1 : 0;
   const LevelCfg cfg = level_cfg(a.level);
   SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
 #ifdef FRA_DIAG_STOP
@@ -384,7 +388,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_an
   {
     const NormParams np = norm_params(st, a.norm[fr.stream]);
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
-    load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax);
+    load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -1249,7 +1253,21 @@ hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s) {
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
 #define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
-  if (b32) {
+  if (a.ms && !b32) {
+    // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
+    grid.y = 2;
+    if (ml == 0) FRA_LAUNCH(false, 0);
+    else if (ml == 8) FRA_LAUNCH(false, 8);
+    else FRA_LAUNCH(false, 12);
+    JobArgs as = a;
+    as.c_base = 2;
+    grid.y = 2;
+#define FRA_LAUNCH_S(M) k_analyze<true, M><<<grid, kThreads, 0, s>>>(as, src)
+    if (ml == 0) FRA_LAUNCH_S(0);
+    else if (ml == 8) FRA_LAUNCH_S(8);
+    else FRA_LAUNCH_S(12);
+#undef FRA_LAUNCH_S
+  } else if (b32) {
     if (ml == 0) FRA_LAUNCH(true, 0);
     else if (ml == 8) FRA_LAUNCH(true, 8);
     else FRA_LAUNCH(true, 12);

@@ -380,7 +380,11 @@ static int plan_build(fra_plan* p) {
   else if (j.norm == 24) bps = 32;  // int32 audio -> 32-bps FLAC
   else bps = (j.dtype == FRA_I16 || j.dtype == FRA_U8 || j.dtype == FRA_I8) ? 16 : 32;
   p->b32 = bps == 32;
-  p->cmax = j.channels;
+  // FRA-1 3.1b mid-side for 2-channel 16-bps streams at the levels whose libFLAC preset enables it:
+  // four virtual channels (L, R, M, S) are analysed per frame, k_frame_bytes keeps the cheapest pair
+  const bool ms = j.channels == 2 && bps == 16 && level_cfg(j.level).ms;
+  p->cmax = ms ? 4 : j.channels;
+  const int sbps_max = ms ? bps + 1 : bps;  // side samples carry one more bit
   p->streams.clear();
   p->frames.clear();
   std::map<int, int> win_index;  // block size -> window table index
@@ -404,6 +408,7 @@ static int plan_build(fra_plan* p) {
     st.sample_rate = j.sample_rate > 0 ? j.sample_rate : sample_rate_for_pixels(st.nsamples);
     st.first_frame = (int32_t)nf_total;
     st.frame_number0 = (uint32_t)j.first_frame;
+    st.ms = ms ? 1 : 0;
     const int64_t nfr = (st.nsamples + j.blocksize - 1) / j.blocksize;
     st.nframes = (int32_t)nfr;
     if (st.nsamples > 0) {
@@ -429,7 +434,7 @@ static int plan_build(fra_plan* p) {
         fr.win = idx;
       } else fr.win = it->second;
       p->frames.push_back(fr);
-      out_cap += 16 + 2 + (size_t)j.channels * ((size_t)fr.n * bps / 8 + 8);
+      out_cap += 16 + 2 + (size_t)j.channels * ((size_t)fr.n * sbps_max / 8 + 8);
     }
     nf_total += nfr;
     p->streams.push_back(st);
@@ -552,7 +557,7 @@ static int plan_build(fra_plan* p) {
     for (auto& e : p->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   // per-subframe slots for the encoded subframes (k_analyze -> k_assemble)
-  p->tmp_stride = ((int64_t)j.blocksize * bps + 64 + 31) / 32 + 4;
+  p->tmp_stride = ((int64_t)j.blocksize * sbps_max + 64 + 31) / 32 + 4;
   HIPCHK(hipMalloc(&p->d_tmp, sizeof(uint32_t) * (size_t)p->tmp_stride * std::max(1, nfr) * p->cmax));
   HIPCHK(hipMalloc(&p->d_fmeta, sizeof(uint32_t) * kMetaWords * std::max(1, nfr)));
   {
@@ -589,6 +594,8 @@ static int plan_build(fra_plan* p) {
   a.blocksize = j.blocksize;
   a.level = j.level;
   a.nwin = std::max(1, p->nwin);
+  a.ms = ms ? 1 : 0;
+  a.c_base = 0;
   for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
   {  // second buffer set for cross-execute pipelining
     const char* ev = getenv("FRA_PIPE");

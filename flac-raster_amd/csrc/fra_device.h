@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "fra_internal.h"
 
 #pragma clang fp contract(off)
@@ -116,17 +118,13 @@ struct alignas(sizeof(T) * V) VecT {
 // host checked that no vector straddles a row and all are aligned: JobArgs::vec8), thread t owns
 // vectors t + 256k; otherwise one element per lane, samples t + 256k.  Returns per-thread OR/min/max.
 template <int SRC, bool VEC, typename SmpT>
-__device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                               const NormParams& np, const int32_t* lut, SmpT* smp, uint32_t& orv,
-                                               int32_t& vmin, int32_t& vmax) {
+__device__ __forceinline__ void load_raw_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                           typename RawType<SRC>::T (&raw)[kMaxBlock / kThreads]) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
   constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
   const T* src = (const T*)base;
   const int n = fr.n, w = st.width, t = threadIdx.x;
-  // sample index of raw[k]
-  auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
-  T raw[K];
   if constexpr (VEC) {
     using VT = VecT<T, V>;
     int col = fr.col0 + t * V, row = fr.row0;
@@ -184,6 +182,65 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
     }
   }
   }
+}
+// FRA-1 3.1b: the mid (L + R) >> 1 (msmode 1) or side L - R (msmode 2) of channels 0 and 1 into smp
+// (32-bit instance only; |l|, |r| < 2^15 since mid-side streams are 16-bps).  Channel 0 is parked in this
+// thread's own smp slots, then combined with channel 1.
+template <int SRC, bool VEC>
+__device__ __forceinline__ void load_mid_side_t(const void* base, const StreamDev& st, const FrameDev& fr,
+                                             const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
+                                             int32_t& vmin, int32_t& vmax, int msmode) {
+  using T = typename RawType<SRC>::T;
+  constexpr int K = kMaxBlock / kThreads;
+  constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
+  constexpr bool kLutType = SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16;
+  const int n = fr.n, t = threadIdx.x;
+  auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
+  auto audio = [&](T r) -> int32_t {
+    if (kLutType && lut) return lut[(int)r - (int)np.mn];
+    return np.mode == 0 ? (int32_t)r : norm_sample<SRC>((double)r, np);
+  };
+  T raw[K];
+  load_raw_t<SRC, VEC, int32_t>(base, st, fr, 0, raw);
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = sidx_of(k);
+    if (i < n) smp[sidx(i)] = audio(raw[k]);
+  }
+  load_raw_t<SRC, VEC, int32_t>(base, st, fr, 1, raw);
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = sidx_of(k);
+    if (i < n) {
+      const int32_t l = smp[sidx(i)], r = audio(raw[k]);
+      const int32_t v = msmode == 1 ? ((l + r) >> 1) : l - r;
+      smp[sidx(i)] = v;
+      orv |= (uint32_t)v;
+      vmin = min(vmin, v);
+      vmax = max(vmax, v);
+    }
+  }
+}
+// Load channel c of frame fr into smp[0..n) as audio integers (LUT / float64 normalisation, or raw
+// ints when norm == 0): all of a thread's loads are issued before any is consumed.  Returns
+// per-thread OR/min/max.  msmode != 0: the mid-side virtual channels (32-bit instance).
+template <int SRC, bool VEC, typename SmpT>
+__device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                               const NormParams& np, const int32_t* lut, SmpT* smp, uint32_t& orv,
+                                               int32_t& vmin, int32_t& vmax, int msmode) {
+  if constexpr (std::is_same<SmpT, int32_t>::value) {
+    if (msmode) {
+      load_mid_side_t<SRC, VEC>(base, st, fr, np, lut, smp, orv, vmin, vmax, msmode);
+      return;
+    }
+  }
+  using T = typename RawType<SRC>::T;
+  constexpr int K = kMaxBlock / kThreads;
+  constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
+  const int n = fr.n, t = threadIdx.x;
+  auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
+  T raw[K];
+  load_raw_t<SRC, VEC, SmpT>(base, st, fr, c, raw);
   if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
     if (lut) {  // <= 16-bit integers: the normalised sample of value mn + d is lut[d] (k_norm_lut)
       const int mnint = (int)np.mn;
@@ -220,28 +277,28 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
 template <typename SmpT>
 __device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const StreamDev& st, const FrameDev& fr,
                                              int c, const NormParams& np, const int32_t* lut, SmpT* smp,
-                                             uint32_t& orv, int32_t& vmin, int32_t& vmax) {
+                                             uint32_t& orv, int32_t& vmin, int32_t& vmax, int msmode) {
   if (vec8) {
     switch (src) {  // wave-uniform dispatch; f64 never takes the vector path
-      case ST_U8: load_channel_t<ST_U8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I8: load_channel_t<ST_I8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_U16: load_channel_t<ST_U16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I16: load_channel_t<ST_I16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_U32: load_channel_t<ST_U32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_I32: load_channel_t<ST_I32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
-      case ST_F32: load_channel_t<ST_F32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); return;
+      case ST_U8: load_channel_t<ST_U8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I8: load_channel_t<ST_I8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_U16: load_channel_t<ST_U16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I16: load_channel_t<ST_I16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_U32: load_channel_t<ST_U32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I32: load_channel_t<ST_I32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_F32: load_channel_t<ST_F32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
       default: break;
     }
   }
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_channel_t<ST_U8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I8: load_channel_t<ST_I8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U16: load_channel_t<ST_U16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I16: load_channel_t<ST_I16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_U32: load_channel_t<ST_U32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_I32: load_channel_t<ST_I32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    case ST_F32: load_channel_t<ST_F32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
-    default: load_channel_t<ST_F64, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax); break;
+    case ST_U8: load_channel_t<ST_U8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I8: load_channel_t<ST_I8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_U16: load_channel_t<ST_U16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I16: load_channel_t<ST_I16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_U32: load_channel_t<ST_U32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I32: load_channel_t<ST_I32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_F32: load_channel_t<ST_F32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    default: load_channel_t<ST_F64, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
   }
 }
 
@@ -742,7 +799,7 @@ __host__ __device__ inline int utf8_len(uint32_t v) {
   if (v < 0x4000000) return 5;
   return 6;
 }
-__device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameDev& fr) {
+__device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameDev& fr, int chan_code) {
   int bsx, srx, srv;
   const int bc = bs_code(fr.n, &bsx);
   const int sc = sr_code(st.sample_rate, &srx, &srv);
@@ -750,7 +807,7 @@ __device__ inline int frame_header(uint8_t* h, const StreamDev& st, const FrameD
   h[p++] = 0xFF;
   h[p++] = 0xF8;
   h[p++] = (uint8_t)((bc << 4) | sc);
-  h[p++] = (uint8_t)(((st.channels - 1) << 4) | (bps_code(st.bps) << 1));
+  h[p++] = (uint8_t)((chan_code << 4) | (bps_code(st.bps) << 1));
   const uint32_t v = (uint32_t)fr.index + st.frame_number0;
   const int nb = utf8_len(v);
   if (nb == 1) h[p++] = (uint8_t)v;

@@ -36,16 +36,18 @@ FRA_HD int sidx(int i) { return kSmpStride + i + ((i >> 4) << 2); }
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {
   int32_t max_lpc, max_porder, nsub;
+  int32_t ms;  // mid-side stereo column (levels 1, 2, 4-8)
 };
 FRA_HD LevelCfg level_cfg(int level) {
   switch (level < 0 ? 0 : (level > 8 ? 8 : level)) {
-    case 0: case 1: case 2: return {0, 3, 0};
-    case 3: return {6, 4, 1};
-    case 4: return {8, 4, 1};
-    case 5: return {8, 5, 1};
-    case 6: return {8, 6, 2};
-    case 7: return {12, 6, 2};
-    default: return {12, 6, 3};
+    case 0: return {0, 3, 0, 0};
+    case 1: case 2: return {0, 3, 0, 1};
+    case 3: return {6, 4, 1, 0};
+    case 4: return {8, 4, 1, 1};
+    case 5: return {8, 5, 1, 1};
+    case 6: return {8, 6, 2, 1};
+    case 7: return {12, 6, 2, 1};
+    default: return {12, 6, 3, 1};
   }
 }
 FRA_HD int num_windows(int nsub) {
@@ -136,7 +138,7 @@ struct StreamDev {
   int32_t first_frame, nframes;
   int64_t nsamples;      // per channel (= width*height)
   uint32_t frame_number0;  // FLAC frame number of the stream's first frame (pyflac shim: blocks already emitted)
-  uint32_t pad_;
+  int32_t ms;            // FRA-1 3.1b mid-side: virtual channels 0 L, 1 R, 2 M = (L+R)>>1, 3 S = L-R (bps+1)
 };
 
 struct FrameDev {
@@ -204,6 +206,8 @@ struct JobArgs {
   int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
+  int32_t ms;              // the plan's streams use mid-side (then cmax = 4 virtual channels)
+  int32_t c_base;          // k_analyze: first (virtual) channel of this launch (blockIdx.y + c_base)
 };
 
 }  // namespace fra

@@ -168,8 +168,21 @@ __global__ void k_frame_bytes(JobArgs a) {
   const int g = a.frame_base + i;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
+  // FRA-1 3.1b: a mid-side stream keeps the first minimum of L+R, L+S, S+R, M+S (virtual channels 0..3)
+  int chan_code = st.channels - 1, va = 0, vb = 1;
+  if (st.ms) {
+    const SfDesc* sd = a.sf + (size_t)g * a.cmax;
+    const uint64_t bl = sd[0].bits, br = sd[1].bits, bm = sd[2].bits, bs = sd[3].bits;
+    const uint64_t tot[4] = {bl + br, bl + bs, bs + br, bm + bs};
+    int best = 0;
+    for (int k = 1; k < 4; k++)
+      if (tot[k] < tot[best]) best = k;
+    chan_code = best == 0 ? 1 : 7 + best;  // 1 independent, 8 left/side, 9 side/right, 10 mid/side
+    va = best == 0 ? 0 : (best == 1 ? 0 : (best == 2 ? 3 : 2));
+    vb = best == 0 ? 1 : (best == 1 ? 3 : (best == 2 ? 1 : 3));
+  }
   uint8_t h[4 * kHdrWords];
-  int hl = frame_header(h, st, fr);
+  int hl = frame_header(h, st, fr, chan_code);
   uint32_t c8 = 0;  // CRC-8, poly x^8+x^2+x+1, init 0 (RFC 9639 9.1.8)
   for (int i = 0; i < hl; i++) {
     c8 ^= h[i];
@@ -179,6 +192,8 @@ __global__ void k_frame_bytes(JobArgs a) {
   uint32_t* m = a.fmeta + (size_t)g * kMetaWords;
   uint32_t w[kHdrWords] = {};
   for (int b = 0; b < hl; b++) w[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
+  // header <= 16 bytes (words 0-3); word kHdrWords - 1 carries the slot of output channels 0 and 1
+  w[kHdrWords - 1] = (uint32_t)va | ((uint32_t)vb << 8);
 #pragma unroll
   for (int j = 0; j < kHdrWords; j++) m[j] = w[j];
   uint32_t bits = (uint32_t)hl * 8;
@@ -186,7 +201,8 @@ __global__ void k_frame_bytes(JobArgs a) {
   m[kHdrWords + 1] = bits;
 #pragma unroll
   for (int c = 0; c < kMaxChannels; c++) {
-    if (c < st.channels) bits += a.sf[(size_t)g * a.cmax + c].bits;
+    const int vc = c == 0 ? va : (c == 1 ? vb : c);
+    if (c < st.channels) bits += a.sf[(size_t)g * a.cmax + vc].bits;
     m[kHdrWords + 2 + c] = c < st.channels ? bits : 0xFFFFFFFFu;
   }
   a.frame_bytes[g] = ((uint64_t)(bits + 7) >> 3) + 2;

@@ -102,6 +102,9 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   const int pad = (int)((kThreads - (NQ % kThreads)) % kThreads);
   const int64_t kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
+  // slot of output channels 0 / 1 (k_frame_bytes: identity unless a mid-side assignment was chosen)
+  const uint32_t smap = C == 2 ? (uint32_t)__builtin_amdgcn_readfirstlane(gmeta[kHdrWords - 1]) : 0u;
+  auto vslot = [&](int oc) -> int { return C == 2 ? (int)((smap >> (8 * oc)) & 0xFFu) : oc; };
 #ifdef FRA_GUARD
   const uint64_t TOT = a.out_cap;  // frame_off[nframes_total] is final only after the last frame group
   const uint64_t SLOTW = (uint64_t)a.nframes_total * a.cmax * a.tmp_stride;
@@ -133,7 +136,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
       const uint32_t take = (uint32_t)min<int64_t>(32 - filled, (int64_t)seg[s + 1] - bp);
       const uint32_t rel = (uint32_t)(bp - seg[s]);
       const uint32_t v =
-          s == 0 ? bits_at(hdrw, rel, (int)take) : bits_at(slots + (size_t)(s - 1) * a.tmp_stride, rel, (int)take);
+          s == 0 ? bits_at(hdrw, rel, (int)take) : bits_at(slots + (size_t)vslot(s - 1) * a.tmp_stride, rel, (int)take);
       res |= take == 32 ? v : (v << (32 - filled - (int)take));
       filled += (int)take;
       bp += take;
@@ -162,7 +165,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
         for (int i = 2; i <= kMaxChannels + 1; i++) sgi += (b >= sg[i]) ? 1 : 0;
         if (b + 128 <= sg[sgi + 1]) {
           const uint32_t rel = b - sg[sgi];
-          const uint32_t* src = slots + (size_t)(sgi - 1) * a.tmp_stride + (rel >> 5);
+          const uint32_t* src = slots + (size_t)vslot(sgi - 1) * a.tmp_stride + (rel >> 5);
           GUARD((uint64_t)(src + 4 - a.tmp) < SLOTW && sgi - 1 < C, "g %d slot read sgi %d rel %u\n", g, sgi, rel);
           uint4 v4;
           __builtin_memcpy(&v4, src, 16);

@@ -173,7 +173,7 @@ typedef struct {
   int max_lpc;
   int max_porder;
   int nsub;     /* 0 = no LPC, 1 = tukey(0.5), 2/3 = subdivide_tukey(2/3) */
-  int stereo;   /* mid-side tried for C == 2 (not applied in FRA-1: independent channels) */
+  int stereo;   /* mid-side stereo tried for C == 2 (FRA-1 3.1b: streams of <= 16 bps) */
 } level_cfg;
 static const level_cfg LEVELS[9] = {
     {0, 3, 0, 0}, {0, 3, 0, 1}, {0, 3, 0, 1}, {6, 4, 1, 0}, {8, 4, 1, 1},
@@ -754,6 +754,10 @@ typedef struct {
   int64_t type_count[4];
 } ora_stats;
 
+/* test hook: 0 disables FRA-1 3.1b (independent channels only), to report mid-side's size gain */
+static int ora_stereo_enabled = 1;
+ORA_API void ora_set_stereo(int enable) { ora_stereo_enabled = enable != 0; }
+
 static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps, int sr, int blocksize,
                           int level, int64_t *frame_bytes /* optional */, int32_t *sf_info /* optional, 4 per sf */) {
   const level_cfg *cfg = &LEVELS[level < 0 ? 0 : level > 8 ? 8 : level];
@@ -767,21 +771,47 @@ static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps,
   float *winfull = nwin ? (float *)malloc(sizeof(float) * nwin * blocksize) : NULL;
   float *winpart = nwin ? (float *)malloc(sizeof(float) * nwin * blocksize) : NULL;
   if (nwin) ora_window_set(winfull, blocksize, cfg->nsub);
-  sf_t *d = (sf_t *)malloc(sizeof(sf_t) * C);
+  /* FRA-1 3.1b mid-side stereo: 2-channel streams of <= 16 bps at the levels whose libFLAC preset
+   * enables it (sonos-pyflac.txt:6926-6934): virtual channels 0 L, 1 R, 2 M = (L + R) >> 1,
+   * 3 S = L - R (bps + 1 bits); the frame keeps the first minimum of L+R, L+S, S+R, M+S. */
+  const int ms = C == 2 && bps <= 16 && cfg->stereo && ora_stereo_enabled;
+  const int V = ms ? 4 : C;
+  int64_t *rb2 = ms ? (int64_t *)realloc(rb, sizeof(int64_t) * V * blocksize) : rb;
+  int64_t *sh2 = ms ? (int64_t *)realloc(sh, sizeof(int64_t) * V * blocksize) : sh;
+  rb = rb2;
+  sh = sh2;
+  sf_t *d = (sf_t *)malloc(sizeof(sf_t) * V);
   for (int64_t f = 0; f < nframes; f++) {
     int n = (int)((N - f * blocksize) < blocksize ? (N - f * blocksize) : blocksize);
     winset_t ws = {nwin, n, winfull};
     if (nwin && n != blocksize) { ora_window_set(winpart, n, cfg->nsub); ws.win = winpart; }
-    for (int c = 0; c < C; c++) {
-      for (int i = 0; i < n; i++) s_in[i] = x[(f * blocksize + i) * C + c];
-      analyze_subframe(s_in, n, bps, cfg, &ws, &d[c], sh + (size_t)c * blocksize, r, rb + (size_t)c * blocksize, wf);
+    for (int c = 0; c < V; c++) {
+      int cb = bps;
+      for (int i = 0; i < n; i++) {
+        const int64_t l = x[(f * blocksize + i) * C], rr = C > 1 ? x[(f * blocksize + i) * C + 1] : 0;
+        if (!ms || c < 2) s_in[i] = x[(f * blocksize + i) * C + c];
+        else if (c == 2) s_in[i] = (l + rr) >> 1;
+        else s_in[i] = l - rr;
+      }
+      if (ms && c == 3) cb = bps + 1;  /* the side channel */
+      analyze_subframe(s_in, n, cb, cfg, &ws, &d[c], sh + (size_t)c * blocksize, r, rb + (size_t)c * blocksize, wf);
       if (d[c].type == 0) { /* constant: analysis returned before filling the shifted copy */
         for (int i = 0; i < n; i++) sh[(size_t)c * blocksize + i] = s_in[i];
       }
-      if (sf_info) {
+      if (sf_info && c < C) {
         int32_t *o = sf_info + ((f * C + c) * 4);
         o[0] = d[c].type; o[1] = d[c].order; o[2] = d[c].porder; o[3] = (int32_t)d[c].bits;
       }
+    }
+    int chan_code = C - 1, ca = 0, cbch = 1;
+    if (ms) {
+      const uint64_t tot[4] = {d[0].bits + d[1].bits, d[0].bits + d[3].bits, d[3].bits + d[1].bits,
+                               d[2].bits + d[3].bits};
+      int best = 0;
+      for (int k = 1; k < 4; k++)
+        if (tot[k] < tot[best]) best = k;
+      static const int codes[4] = {1, 8, 9, 10}, cha[4] = {0, 0, 3, 2}, chb[4] = {1, 3, 1, 3};
+      chan_code = codes[best]; ca = cha[best]; cbch = chb[best];
     }
     /* frame header */
     uint64_t fstart = bw->bits;
@@ -791,7 +821,7 @@ static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps,
     bw_put(bw, 0xFFF8, 16);
     bw_put(bw, (uint64_t)bcode, 4);
     bw_put(bw, (uint64_t)scode, 4);
-    bw_put(bw, (uint64_t)(C - 1), 4);
+    bw_put(bw, (uint64_t)chan_code, 4);
     bw_put(bw, (uint64_t)bps_code(bps), 3);
     bw_put(bw, 0, 1);
     put_utf8(bw, (uint64_t)f);
@@ -799,7 +829,8 @@ static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps,
     if (srx) bw_put(bw, (uint64_t)srv, srx);
     size_t hb = (size_t)((bw->bits - fstart) / 8);
     bw_put(bw, ora_crc8(bw->buf + fstart / 8, hb), 8);
-    for (int c = 0; c < C; c++) {
+    for (int k = 0; k < C; k++) {
+      const int c = (C == 2) ? (k == 0 ? ca : cbch) : k;
       write_subframe(bw, &d[c], sh + (size_t)c * blocksize, rb + (size_t)c * blocksize, n);
     }
     bw_align(bw);

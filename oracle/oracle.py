@@ -72,6 +72,7 @@ def lib():
     L.ora_det_log2.argtypes = [C.c_double]
     L.ora_det_log2.restype = C.c_double
     L.ora_sample_rate_for_pixels.argtypes = [C.c_int64]
+    L.ora_set_stereo.argtypes = [C.c_int]
     _LIB = L
     return L
 
@@ -111,6 +112,11 @@ def crc8(b: bytes) -> int:
 def crc16(b: bytes) -> int:
     a = np.frombuffer(b, dtype=np.uint8)
     return lib().ora_crc16(_ptr(a), a.size)
+
+
+def set_stereo(enable: bool):
+    """FRA-1 3.1b mid-side stereo on/off (test hook: report the size gain over independent channels)."""
+    lib().ora_set_stereo(1 if enable else 0)
 
 
 def encode(samples: np.ndarray, sample_rate: int, level: int = 5, blocksize: int = 4096,

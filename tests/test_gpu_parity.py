@@ -217,3 +217,32 @@ def test_32bps_verbatim_and_wasted_bits(blocksize):
         assert frames == O.encode(a, 44100, level=8, blocksize=blocksize, with_header=False)
         dec, _, _, _ = O.decode(O.stream_header(2, 32, 44100, blocksize) + frames)
         assert np.array_equal(dec, a)
+
+
+@pytest.mark.parametrize("level", [0, 1, 3, 5, 8])
+def test_two_band_mid_side(golden_dir, level):
+    """FRA-1 3.1b: 2-band rasters (16-bps streams) choose among L/R, L/S, S/R, M/S per frame at the
+    levels whose libFLAC preset enables mid-side; the side channel (17-bit samples) runs on the 32-bit
+    instance.  Ragged tiles cover partial frames."""
+    data, _ = read_geotiff(golden_dir / "sample_rgb.tif")
+    check_windows(np.ascontiguousarray(data[:2]), [(0, 0, 256, 256), (7, 3, 100, 91)], level, 16)
+    r = synth_window(4, 31, 2, 700, 900)
+    check_windows(r, tiles(700, 900, 512), level, 16)
+    c = r.copy()
+    c[1] = c[0]  # identical bands: the side channel is all zeros (CONSTANT)
+    check_windows(c, [(0, 0, 300, 900)], level, 16)
+
+
+def test_two_channel_pyflac_path_mid_side():
+    rng = np.random.default_rng(5)
+    base = np.cumsum(rng.integers(-40, 41, size=(30000, 1)), axis=0)
+    a = np.clip(np.concatenate([base, base + rng.integers(-9, 10, size=(30000, 1))], axis=1), -32768, 32767)
+    a = a.astype(np.int16)
+    for level in (2, 5, 8):
+        info, frames = N.encode_interleaved(a, 44100, level=level)
+        assert frames == O.encode(a, 44100, level=level, with_header=False)
+        dec, _, _, _ = O.decode(O.stream_header(2, 16, 44100, 4096) + frames)
+        assert np.array_equal(dec, a.astype(np.int32))
+    a32 = a.astype(np.int32) * 97  # 32-bps: independent channels only
+    info, frames = N.encode_interleaved(a32, 44100, level=5)
+    assert frames == O.encode(a32, 44100, level=5, with_header=False)

@@ -139,3 +139,27 @@ def test_window_and_lpc_primitives():
     assert n == 8 and np.all(np.diff(err) <= 0)
     q, sh = O.quantize(lp[1], 2, 12)
     assert 0 <= sh <= 15 and np.all(np.abs(q) < 2048)
+
+
+def test_oracle_mid_side_round_trip_and_gain(golden_dir):
+    """FRA-1 3.1b on the CPU: 2-channel 16-bps streams decode bit-exactly (oracle and product decoders)
+    and are never larger than independent coding (the side/mid choice is a per-frame minimum)."""
+    import numpy as np
+
+    import oracle as O
+    from flac_raster import _native as N
+    from flac_raster.tiff import read_geotiff
+
+    rgb, _ = read_geotiff(golden_dir / "sample_rgb.tif")
+    for bands in ((0, 1), (1, 2)):
+        a, _, _ = O.normalize(rgb[list(bands)].transpose(1, 2, 0).reshape(-1, 2), 16)
+        for level in (1, 5, 8):
+            ms = O.encode(a, 44100, level=level)
+            O.set_stereo(False)
+            try:
+                ind = O.encode(a, 44100, level=level)
+            finally:
+                O.set_stereo(True)
+            assert len(ms) <= len(ind)
+            assert np.array_equal(O.decode(ms)[0], a.astype(np.int32))
+            assert np.array_equal(N.decode(ms)[0], a.astype(np.int32))
