@@ -358,12 +358,12 @@ template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  const int g = a.frame_base + (int)blockIdx.x, c = a.c_base + (int)blockIdx.y, t = threadIdx.x, lane = t & 63,
-            wv = t >> 6;
+  const int g = a.frame_base + (int)blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
-  // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; M and S (bps + 1 bits) are
-  // analysed by the 32-bit instance (launched with c_base 2), L and R by the 16-bit one
+  // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
+  // 16-bit instance, M and S (bps + 1 bits) by the 32-bit one, whose grid rows 0-1 are channels 2-3
+  const int c = (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
   if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
   const int n = fr.n;
   const int bps = st.bps + ((st.ms && c == 3) ? 1 : 0);
@@ -1247,26 +1247,21 @@ read_x28(S.smp, t, x);
   for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
 }
 
-hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s) {
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
 #define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
-  if (a.ms && !b32) {
+  if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
     grid.y = 2;
     if (ml == 0) FRA_LAUNCH(false, 0);
     else if (ml == 8) FRA_LAUNCH(false, 8);
     else FRA_LAUNCH(false, 12);
-    JobArgs as = a;
-    as.c_base = 2;
-    grid.y = 2;
-#define FRA_LAUNCH_S(M) k_analyze<true, M><<<grid, kThreads, 0, s>>>(as, src)
-    if (ml == 0) FRA_LAUNCH_S(0);
-    else if (ml == 8) FRA_LAUNCH_S(8);
-    else FRA_LAUNCH_S(12);
-#undef FRA_LAUNCH_S
+    if (ml == 0) FRA_LAUNCH(true, 0);
+    else if (ml == 8) FRA_LAUNCH(true, 8);
+    else FRA_LAUNCH(true, 12);
   } else if (b32) {
     if (ml == 0) FRA_LAUNCH(true, 0);
     else if (ml == 8) FRA_LAUNCH(true, 8);

@@ -31,7 +31,7 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
                          hipStream_t s);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
-hipError_t launch_analyze(int src, bool b32, const JobArgs& a, hipStream_t s);
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
@@ -594,8 +594,6 @@ static int plan_build(fra_plan* p) {
   a.blocksize = j.blocksize;
   a.level = j.level;
   a.nwin = std::max(1, p->nwin);
-  a.ms = ms ? 1 : 0;
-  a.c_base = 0;
   for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
   {  // second buffer set for cross-execute pipelining
     const char* ev = getenv("FRA_PIPE");
@@ -741,7 +739,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   JobArgs ga = a;
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
-  HIPCHK(launch_analyze(p->src, p->b32, ga, st));
+  HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st));
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   HIPCHK(launch_frame_bytes(ga, st));
   if (nf > 0) {

@@ -206,8 +206,6 @@ struct JobArgs {
   int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
-  int32_t ms;              // the plan's streams use mid-side (then cmax = 4 virtual channels)
-  int32_t c_base;          // k_analyze: first (virtual) channel of this launch (blockIdx.y + c_base)
 };
 
 }  // namespace fra
