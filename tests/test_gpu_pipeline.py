@@ -103,3 +103,42 @@ def test_pinned_pool_reuse():
     b = N.pinned_empty((1 << 20) - 100, np.uint8)
     assert b.ctypes.data == p and N.is_pinned(b)
     N.release_pinned_pool()
+
+
+def test_cross_execute_pipelining_buffers():
+    """A plan large enough for cross-execute pipelining (>= 4096 frames: k_assemble of execute k on its own
+    stream while execute k+1 analyses into the other buffer set) gives the same bytes on every execute,
+    after a drain into the timing mode and into the host pipeline, and after set_raster."""
+    H, W = 4096, 4096
+    r = synth_window(3, 77, 1, H, W)
+    wins = calculate_tiles(H, W, 512)
+    ctx = N.default_context(0)
+    dev = ctx.alloc(r.nbytes)
+    try:
+        ctx.h2d(dev, r)
+        plan = N.Plan(ctx, dev, True, r.dtype, 1, (H * W, W, 1), wins, 5, 4096, 16)
+        try:
+            outs = []
+            for _ in range(3):  # buffer sets 0, 1, 0
+                plan.execute()
+                plan.sync()
+                outs.append(plan.download())
+            assert all(o[1] == outs[0][1] for o in outs)
+            assert all(_table(o[0]) == _table(outs[0][0]) for o in outs)
+            plan.execute()
+            plan.execute()  # two in flight, then the timing mode drains them
+            plan.enable_timing(True)
+            plan.execute()
+            plan.sync()
+            assert plan.download()[1] == outs[0][1]
+            plan.enable_timing(False)
+            plan.execute()
+            cap, _ = plan.capacity()
+            out = np.empty(cap, np.uint8)
+            total = plan.encode_host(r, out)  # drains the pipelined execute, then the host bands
+            assert bytes(out[:total]) == outs[0][1]
+            assert plan.frame_offsets(sum(i.nframes for i in outs[0][0]))[-1] == total
+        finally:
+            plan.close()
+    finally:
+        ctx.free(dev)
