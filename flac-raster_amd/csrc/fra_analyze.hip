@@ -359,6 +359,10 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_an
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   const int g = a.frame_base + (int)blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the
+  // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
+  // the encoder's scan) keeps the physical wave index wv
+  const int rw = (wv + (int)((blockIdx.x + blockIdx.y) & 3)) & 3;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
@@ -571,25 +575,25 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_an
       // two FIXED candidates are searched meanwhile on the next two waves (psum is complete since the
       // autocorrelation barrier)
       const int nldw = (a.nwin + 3) >> 2;
-      if (early && (wv == nldw || wv == nldw + 1)) {
+      if (early && (rw == nldw || rw == nldw + 1)) {
         int g1, g2;
         fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
-        if (wv == nldw && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
-        const int m = wv == nldw ? g1 : g2;
+        if (rw == nldw && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
+        const int m = rw == nldw ? g1 : g2;
         if (m >= 0) {
           const int pm = max_porder(n, m, cfg.max_porder);
           uint64_t best = 0;
           int bp = pm;
-          porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, m, lane, best, bp, S.kbest[m]);
+          porder_search(S.u.psum[m], S.nu.node[rw], P, pm, n, m, lane, best, bp, S.kbest[m]);
           if (lane == 0) {
             S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
             S.mporder[m] = bp;
           }
         }
       }
-      if (wv < nldw) {
+      if (rw < nldw) {
         const int gw = lane >> 4, lo = lane & 15;
-        const int wi = 4 * wv + gw;
+        const int wi = 4 * rw + gw;
         const bool gon = wi < a.nwin;
         const int ws = gon ? wi : 0;
         double ac[MAXLAG + 1];
@@ -731,15 +735,15 @@ read_x28(S.smp, t, x);
   int fg1 = -1, fg2 = -1;
   if (!early) {  // FIXED candidates (3.7): excluded orders are invalidated before the winner barrier
     fixed_guess2(S.u.psum, S.mvalid, P, lane, fg1, fg2);
-    if (wv == 0 && lane < 5 && lane != fg1 && lane != fg2) S.mvalid[lane] = 0;
+    if (rw == 0 && lane < 5 && lane != fg1 && lane != fg2) S.mvalid[lane] = 0;
   }
-  for (int m = (early ? 5 : 0) + wv; m < nmod; m += 4) {
+  for (int m = (early ? 5 : 0) + rw; m < nmod; m += 4) {
     if (!S.mvalid[m] || (m < 5 && m != fg1 && m != fg2)) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], S.nu.node[wv], P, pm, n, o, lane, best, bp, S.kbest[m]);
+    porder_search(S.u.psum[m], S.nu.node[rw], P, pm, n, o, lane, best, bp, S.kbest[m]);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
@@ -748,8 +752,8 @@ read_x28(S.smp, t, x);
   {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share
     static_assert(kMaxPart * 3 <= 2 * (2 * kMaxPart), "esum2 inside node[0..1]");
     unsigned long long* ez = &S.nu.e.esum2[0][0];
-    const int e1 = min(kMaxPart * 3, (wv + 1) * 2 * kMaxPart);
-    for (int i = wv * 2 * kMaxPart + lane; i < e1; i += 64) ez[i] = 0ull;
+    const int e1 = min(kMaxPart * 3, (rw + 1) * 2 * kMaxPart);
+    for (int i = rw * 2 * kMaxPart + lane; i < e1; i += 64) ez[i] = 0ull;
   }
   __syncthreads();
   FRA_STOP(5)
@@ -879,7 +883,7 @@ read_x28(S.smp, t, x);
       const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
       const bool verbatim = exact >= verb;
       const int kcur = __shfl(bk, pidx, 64);
-      if (wv == 0) {
+      if (rw == 0) {
         if (lane < npp) d->k[lane] = (uint8_t)bk;
         if (lane < kMaxLpc) d->coef[lane] = type == 3 ? S.mcoef[m][lane] : 0;
         if (lane == 0) {
@@ -960,7 +964,7 @@ read_x28(S.smp, t, x);
       return;
     }
   }
-  if (wv == 0) {  // winner = first minimal estimate: argmin over (estimate, model index)
+  if (rw == 0) {  // winner = first minimal estimate: argmin over (estimate, model index)
     uint32_t key = ~0u;
     if (lane < nmod && S.mvalid[lane]) key = (S.mest[lane] << 5) | (uint32_t)lane;
     key = wave_min32(key);
@@ -972,7 +976,7 @@ read_x28(S.smp, t, x);
   // ---- 6. exact Rice bits for the winner (3.9)
   const int m = S.winner;
   const int type = S.mtype[m], o = S.morder[m], sh = S.mshift[m], ps = S.mporder[m];
-  if (wv == 0) {
+  if (rw == 0) {
     uint64_t Sv = lane < (1 << P) ? S.u.psum[m][lane] : 0ull;
     const int smax = P - ps;
     if (smax > 0) Sv = up_add64<0>(Sv);
@@ -1101,7 +1105,7 @@ read_x28(S.smp, t, x);
     }
   }
   __syncthreads();
-  if (wv == 0) {
+  if (rw == 0) {
     const int npp = 1 << ps;
     uint64_t best = 0;
     int bk = 0;

@@ -28,7 +28,7 @@
 
 namespace fra {
 hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, int vec_bytes, int rows, int max_rows,
-                         hipStream_t s);
+                         hipStream_t s, int max_blocks);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
@@ -79,6 +79,7 @@ struct fra_plan {
   int mm_vec = 0, mm_rows = 1, mm_max_rows = 0;  // vectorised k_minmax shape (0 = scalar path)
   bool ld_vec8 = false;  // k_analyze 8-byte sample vectors possible (pointer alignment checked at execute)
   int cmax = 1;
+  int ncu = 256;  // compute units of the device (background grids)
   size_t raster_bytes = 0;
   // device buffers
   void* d_raster_owned = nullptr;
@@ -132,6 +133,15 @@ struct fra_plan {
   hipStream_t pack = nullptr;
   hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
   bool pack_pending[2] = {false, false};
+  // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
+  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set): k_minmax_vec
+  // fits the 32 VGPRs per SIMD that six k_analyze workgroups leave free, so it co-resides
+  NormDev* norm2[2] = {};
+  int32_t* lut2[2] = {};
+  hipStream_t nstream = nullptr;
+  hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
+  bool ana_pending[2] = {false, false};
+  bool raster_dirty = false;  // a host raster copy on the plan's stream the norm stream must wait for
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -256,7 +266,11 @@ int fra_ctx_create(int device, fra_ctx** out) {
   fra_ctx* c = new (std::nothrow) fra_ctx();
   if (!c) return set_err(FRA_E_NOMEM, "out of host memory");
   c->device = device;
-  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  // the highest stream priority: background kernels of pipelined plans (low-priority streams) fill the
+  // CU resources k_analyze leaves free rather than competing for them
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+  hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
   if (e != hipSuccess) { delete c; return set_err(FRA_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
   *out = c;
   return FRA_OK;
@@ -275,7 +289,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_raster_owned);
   (void)hipFree(p->d_streams);
   (void)hipFree(p->d_frames);
-  (void)hipFree(p->d_norm);
+  if (!p->pipe) (void)hipFree(p->d_norm);
   (void)hipFree(p->d_win);
   (void)hipFree(p->d_wrange);
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
@@ -285,14 +299,21 @@ void fra_plan_destroy(fra_plan* p) {
       (void)hipFree(p->foff2[b]);
       (void)hipFree(p->tmp2[b]);
       (void)hipFree(p->fmeta2[b]);
+      (void)hipFree(p->norm2[b]);
+      (void)hipFree(p->lut2[b]);
     }
     p->d_sf = nullptr; p->d_fbytes = nullptr; p->d_foff = nullptr; p->d_tmp = nullptr; p->d_fmeta = nullptr;
+    p->d_norm = nullptr; p->d_lut = nullptr;
   }
   if (p->pack) (void)hipStreamDestroy(p->pack);
+  if (p->nstream) (void)hipStreamDestroy(p->nstream);
   for (int b = 0; b < 2; b++) {
     if (p->ev_scan[b]) (void)hipEventDestroy(p->ev_scan[b]);
     if (p->ev_pack[b]) (void)hipEventDestroy(p->ev_pack[b]);
+    if (p->ev_norm[b]) (void)hipEventDestroy(p->ev_norm[b]);
+    if (p->ev_ana[b]) (void)hipEventDestroy(p->ev_ana[b]);
   }
+  if (p->ev_raster) (void)hipEventDestroy(p->ev_raster);
   (void)hipFree(p->d_sf);
   (void)hipFree(p->d_fbytes);
   (void)hipFree(p->d_foff);
@@ -301,7 +322,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_crctab);
   (void)hipFree(p->d_tmp);
   (void)hipFree(p->d_fmeta);
-  (void)hipFree(p->d_lut);
+  if (!p->pipe) (void)hipFree(p->d_lut);
   (void)hipFree(p->d_gbase);
   for (auto& st : p->aux)
     if (st) (void)hipStreamDestroy(st);
@@ -371,6 +392,11 @@ static void build_host_bands(fra_plan* p, int nfr) {
 }
 
 static int plan_build(fra_plan* p) {
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device) == hipSuccess && ncu > 0)
+      p->ncu = ncu;
+  }
   const fra_job& j = p->job;
   p->src = j.dtype;
   const int nsub = level_cfg(j.level).nsub;
@@ -455,6 +481,7 @@ static int plan_build(fra_plan* p) {
       if (!ok) continue;
       const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(64, 2048 / max_nv));
       if (rows * max_nv * max_nv >= (int64_t(1) << 32)) continue;
+      if (rows * j.row_stride * elem_size(j.dtype) >= (int64_t(1) << 32)) continue;  // 32-bit byte offsets
       p->mm_vec = vb;
       p->mm_rows = (int)rows;
       p->mm_max_rows = 0;
@@ -602,22 +629,40 @@ static int plan_build(fra_plan* p) {
     // leave 32 VGPRs and 7.9 KiB of LDS per CU/SIMD) -- C3 1.610 -> 1.586 ms, C4 2.422 -> 2.408 ms
     const bool want = !(ev && atoi(ev) == 0) && p->groups.size() == 1 && nfr >= 4096;
     const size_t nsf = (size_t)nfr * p->cmax;
+    const size_t nst = std::max<size_t>(1, p->streams.size());
     const size_t extra = sizeof(SfDesc) * nsf + sizeof(uint32_t) * (size_t)p->tmp_stride * nsf +
-                         sizeof(uint32_t) * kMetaWords * nfr + 2 * sizeof(unsigned long long) * (nfr + 1);
+                         sizeof(uint32_t) * kMetaWords * nfr + 2 * sizeof(unsigned long long) * (nfr + 1) +
+                         sizeof(NormDev) * nst + (p->d_lut ? sizeof(int32_t) * (size_t)lut_stride * nst : 0);
     size_t freeb = 0, totalb = 0;
     if (want && hipMemGetInfo(&freeb, &totalb) == hipSuccess && extra <= freeb / 3) {
       p->sf2[0] = p->d_sf; p->tmp2[0] = p->d_tmp; p->fmeta2[0] = p->d_fmeta;
       p->fbytes2[0] = p->d_fbytes; p->foff2[0] = p->d_foff;
+      p->norm2[0] = p->d_norm; p->lut2[0] = p->d_lut;
       p->pipe = true;  // from here on destroy frees through the arrays
+      HIPCHK(hipMalloc(&p->norm2[1], sizeof(NormDev) * nst));
+      HIPCHK(hipMemset(p->norm2[1], 0, sizeof(NormDev) * nst));
+      if (p->d_lut) HIPCHK(hipMalloc(&p->lut2[1], sizeof(int32_t) * (size_t)lut_stride * nst));
+      {  // background streams at the lowest priority (the plan's stream is created at the highest)
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&p->nstream, hipStreamNonBlocking, lo));
+      }
+      HIPCHK(hipEventCreateWithFlags(&p->ev_raster, hipEventDisableTiming));
       HIPCHK(hipMalloc(&p->sf2[1], sizeof(SfDesc) * std::max<size_t>(1, nsf)));
       HIPCHK(hipMalloc(&p->tmp2[1], sizeof(uint32_t) * (size_t)p->tmp_stride * std::max<size_t>(1, nsf)));
       HIPCHK(hipMalloc(&p->fmeta2[1], sizeof(uint32_t) * kMetaWords * nfr));
       HIPCHK(hipMalloc(&p->fbytes2[1], sizeof(unsigned long long) * (nfr + 1)));
       HIPCHK(hipMalloc(&p->foff2[1], sizeof(unsigned long long) * (nfr + 1)));
-      HIPCHK(hipStreamCreateWithFlags(&p->pack, hipStreamNonBlocking));
+      {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&p->pack, hipStreamNonBlocking, lo));
+      }
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&p->ev_pack[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_norm[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_ana[b], hipEventDisableTiming));
       }
     }
   }
@@ -629,22 +674,28 @@ static void use_buffers(fra_plan* p, int b) {
   if (!p->pipe) return;
   p->d_sf = p->sf2[b]; p->d_tmp = p->tmp2[b]; p->d_fmeta = p->fmeta2[b];
   p->d_fbytes = p->fbytes2[b]; p->d_foff = p->foff2[b];
+  p->d_norm = p->norm2[b]; p->d_lut = p->lut2[b];
   p->args.sf = p->d_sf; p->args.tmp = p->d_tmp; p->args.fmeta = p->d_fmeta;
   p->args.frame_bytes = p->d_fbytes; p->args.frame_off = p->d_foff;
+  p->args.norm = p->d_norm; p->args.lut = p->d_lut;
   p->cur = b;
 }
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
   if (!p->pipe) return FRA_OK;
-  for (int b = 0; b < 2; b++)
+  for (int b = 0; b < 2; b++) {
     if (p->pack_pending[b]) {
       HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_pack[b], 0));
       p->pack_pending[b] = false;
     }
+    p->ana_pending[b] = false;  // (analyses run on the plan's stream itself)
+  }
+  p->raster_dirty = false;     // later norm stages run on the plan's stream, after the copy
   use_buffers(p, 0);
   return FRA_OK;
 }
 static int plan_sync_all(fra_plan* p) {
+  if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
   if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));
   return FRA_OK;
@@ -657,8 +708,13 @@ int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
     p->d_raster = raster;
   } else {
     if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
-    if (p->raster_bytes)
+    if (p->raster_bytes) {
       HIPCHK(hipMemcpyAsync(p->d_raster_owned, raster, p->raster_bytes, hipMemcpyHostToDevice, p->ctx->stream));
+      if (p->pipe) {  // the next pipelined norm stage (norm stream) reads the new raster after this copy
+        HIPCHK(hipEventRecord(p->ev_raster, p->ctx->stream));
+        p->raster_dirty = true;
+      }
+    }
     p->d_raster = p->d_raster_owned;
   }
   p->args.raster = p->d_raster;
@@ -718,8 +774,10 @@ static void collect_times(fra_plan* p) {
 static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
                      hipEvent_t ev_pub, hipEvent_t t_norm, hipEvent_t t_ana, hipEvent_t t_scan, int slot = -1,
                      unsigned long long* host_mirror = nullptr, hipStream_t pack_st = nullptr,
-                     hipEvent_t ev_scan = nullptr) {
+                     hipEvent_t ev_scan = nullptr, hipStream_t norm_st = nullptr, hipEvent_t ev_norm = nullptr,
+                     hipEvent_t ev_ana = nullptr) {
   const JobArgs& a = p->args;
+  const hipStream_t nst_s = norm_st ? norm_st : st;  // the normalisation stage's stream
   const int nst = gr.w1 - gr.w0, nf = gr.f1 - gr.f0;
   // the minmax family indexes streams by blockIdx.y: launched per chunk of <= kMaxGridY windows, with the
   // stream/norm/LUT pointers offset to the chunk (grid Y is limited to 65535 on the device)
@@ -731,9 +789,17 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     ma.norm += gr.w0 + c0;
     if (ma.lut) ma.lut += (int64_t)(gr.w0 + c0) * a.lut_stride;
     const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
-    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, st));
-    HIPCHK(launch_norm_finalize(ma, nc, st));
-    HIPCHK(launch_norm_lut(p->src, ma, nc, st));
+    // background norm stage: one workgroup per CU striding over the row blocks (it shares the CUs with
+    // k_analyze instead of filling them)
+    static const int bg_blocks = getenv("FRA_BG_BLOCKS") ? atoi(getenv("FRA_BG_BLOCKS")) : -1;
+    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, nst_s,
+                         norm_st ? (bg_blocks >= 0 ? bg_blocks : p->ncu) : 0));
+    HIPCHK(launch_norm_finalize(ma, nc, nst_s));
+    HIPCHK(launch_norm_lut(p->src, ma, nc, nst_s));
+  }
+  if (norm_st) {
+    HIPCHK(hipEventRecord(ev_norm, norm_st));
+    HIPCHK(hipStreamWaitEvent(st, ev_norm, 0));
   }
   if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
   JobArgs ga = a;
@@ -741,6 +807,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   ga.frame_count = nf;
   HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st));
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
+  if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
   HIPCHK(launch_frame_bytes(ga, st));
   if (nf > 0) {
     size_t tb = p->scan_stride;
@@ -774,10 +841,21 @@ int fra_plan_execute(fra_plan* p) {
     // cross-execute pipelining: this execute's analysis overlaps the previous execute's k_assemble
     const int b = p->cur ^ 1;
     if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(s, p->ev_pack[b], 0));  // execute k-2 is done with set b
+    // one background kernel at a time beside k_analyze: this norm stage after k_assemble of execute k-2
+    // (which runs under the analysis of execute k-1)
+    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_pack[b], 0));
     use_buffers(p, b);
+    // norm stage of this execute on the norm stream: after execute k-2's analysis read set b, and after a
+    // host raster copy enqueued on the plan's stream since the last execute
+    if (p->ana_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_ana[b], 0));
+    if (p->raster_dirty) {
+      HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_raster, 0));
+      p->raster_dirty = false;
+    }
     rc = run_group(p, p->groups[0], 0, 1, s, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
-                   p->ev_scan[b]);
+                   p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
     if (rc) return rc;
+    p->ana_pending[b] = true;
     HIPCHK(hipEventRecord(p->ev_pack[b], p->pack));
     p->pack_pending[b] = true;
     p->executed = true;

@@ -110,55 +110,66 @@ __device__ __forceinline__ double unkey32(uint32_t k) {
 }
 template <int SRC, int V>
 __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const StreamDev* streams, NormDev* nd,
-                                                    int rows) {
+                                                    int rows, int nrb, int nitems) {
   using T = typename RawType<SRC>::T;
   using VT = VecT<T, V>;
-  constexpr int U = 8;
-  const StreamDev st = streams[blockIdx.y];
-  if (st.norm == 0) return;
-  const int r0 = blockIdx.x * rows;
-  if (r0 >= st.height) return;
-  const int nr = min(st.height - r0, rows);
-  const uint32_t nv = (uint32_t)(st.width / V);
-  const uint32_t E = (uint32_t)nr * nv;  // (row, vector) items per band
-  // idx / nv by multiply-high: exact while E * nv < 2^32 (checked on the host); nv == 1 (a window one
-  // vector wide) would wrap the multiplier to 0, so it divides by 1 directly (uniform branch)
-  const uint32_t magic = nv > 1 ? 0xFFFFFFFFu / nv + 1u : 0u;
-  uint32_t kmin = ~0u, kmax = 0u;
-  for (int b = 0; b < st.channels; b++) {
-    const T* base = (const T*)raster + st.base_off + (int64_t)b * st.band_stride + (int64_t)r0 * st.row_stride;
-    for (uint32_t i0 = 0; i0 < E; i0 += 256 * U) {
-      VT x[U];
+  // loads in flight per thread: 48 bytes (<= 32 VGPRs with offsets and keys), 8 loads of narrow vectors
+  constexpr int U = sizeof(VT) >= 16 ? 3 : (sizeof(VT) >= 8 ? 6 : 8);
+  __shared__ uint32_t smn[4], smx[4];
+  const int wv = threadIdx.x >> 6;
+  // items (stream, block of `rows` rows) = (item / nrb, item % nrb); a full grid has one item per
+  // workgroup, the background grid of the pipelined plan (one workgroup per CU) strides over them
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int si = item / nrb;
+    const StreamDev st = streams[si];
+    const int r0 = (item - si * nrb) * rows;
+    if (st.norm == 0 || r0 >= st.height) continue;  // uniform
+    const int nr = min(st.height - r0, rows);
+    const uint32_t nv = (uint32_t)(st.width / V);
+    const uint32_t E = (uint32_t)nr * nv;  // (row, vector) items per band
+    // idx / nv by multiply-high: exact while E * nv < 2^32 (checked on the host); nv == 1 (a window one
+    // vector wide) would wrap the multiplier to 0, so it divides by 1 directly (uniform branch)
+    const uint32_t magic = nv > 1 ? 0xFFFFFFFFu / nv + 1u : 0u;
+    uint32_t kmin = ~0u, kmax = 0u;
+    for (int b = 0; b < st.channels; b++) {
+      // uniform base + 32-bit byte offsets (host: rows * row_stride * itemsize < 2^32): one offset VGPR
+      // per load instead of a 64-bit address pair, so the kernel fits the 32 VGPRs a co-resident
+      // k_analyze leaves free on each SIMD (cross-execute overlap)
+      const char* base =
+          (const char*)((const T*)raster + st.base_off + (int64_t)b * st.band_stride + (int64_t)r0 * st.row_stride);
+      const uint32_t rsb = (uint32_t)st.row_stride * (uint32_t)sizeof(T);
+      for (uint32_t i0 = 0; i0 < E; i0 += 256 * U) {
+        VT x[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) {  // items past E re-read item E-1 (idempotent for min/max)
-        const uint32_t idx = min(i0 + (uint32_t)(u * 256) + threadIdx.x, E - 1);
-        const uint32_t r = nv > 1 ? __umulhi(idx, magic) : idx, v = idx - r * nv;
-        x[u] = *(const VT*)(base + (int64_t)r * st.row_stride + (int64_t)v * V);
-      }
+        for (int u = 0; u < U; u++) {  // items past E re-read item E-1 (idempotent for min/max)
+          const uint32_t idx = min(i0 + (uint32_t)(u * 256) + threadIdx.x, E - 1);
+          const uint32_t r = nv > 1 ? __umulhi(idx, magic) : idx, v = idx - r * nv;
+          x[u] = *(const VT*)(base + (r * rsb + v * (uint32_t)sizeof(VT)));
+        }
 #pragma unroll
-      for (int u = 0; u < U; u++) {
+        for (int u = 0; u < U; u++) {
 #pragma unroll
-        for (int e = 0; e < V; e++) {
-          bool ok;
-          const uint32_t k = key32<SRC>(x[u].v[e], ok);
-          kmin = ok ? min(kmin, k) : kmin;
-          kmax = ok ? max(kmax, k) : kmax;
+          for (int e = 0; e < V; e++) {
+            bool ok;
+            const uint32_t k = key32<SRC>(x[u].v[e], ok);
+            kmin = ok ? min(kmin, k) : kmin;
+            kmax = ok ? max(kmax, k) : kmax;
+          }
         }
       }
     }
-  }
-  kmin = wave_min32(kmin);
-  kmax = ~wave_min32(~kmax);
-  __shared__ uint32_t smn[4], smx[4];
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { smn[wv] = kmin; smx[wv] = kmax; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; w++) { kmin = min(kmin, smn[w]); kmax = max(kmax, smx[w]); }
-    if (kmin <= kmax) {  // at least one non-NaN value
-      atomicMin(&nd[blockIdx.y].mnkey, okey(unkey32<SRC>(kmin)));
-      atomicMax(&nd[blockIdx.y].mxkey, okey(unkey32<SRC>(kmax)));
+    kmin = wave_min32(kmin);
+    kmax = ~wave_min32(~kmax);
+    if ((threadIdx.x & 63) == 0) { smn[wv] = kmin; smx[wv] = kmax; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 4; w++) { kmin = min(kmin, smn[w]); kmax = max(kmax, smx[w]); }
+      if (kmin <= kmax) {  // at least one non-NaN value
+        atomicMin(&nd[si].mnkey, okey(unkey32<SRC>(kmin)));
+        atomicMax(&nd[si].mxkey, okey(unkey32<SRC>(kmax)));
+      }
     }
+    __syncthreads();  // smn/smx reused by the next item
   }
 }
 
@@ -255,14 +266,15 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s) {
 
 // vec_bytes = 16 or 8: vector path (host-checked alignment), rows/max_rows its block shape; 0: scalar
 hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, int vec_bytes, int rows, int max_rows,
-                         hipStream_t s) {
+                         hipStream_t s, int max_blocks) {
   k_norm_init<<<(nstreams + 255) / 256, 256, 0, s>>>(a.norm, nstreams);
   if (vec_bytes == 16 || vec_bytes == 8) {
-    dim3 vgrid((unsigned)((max_rows + rows - 1) / rows), (unsigned)nstreams);
+    const int nrb = (max_rows + rows - 1) / rows, nitems = nrb * nstreams;
+    const unsigned vgrid = (unsigned)(max_blocks > 0 ? std::min(max_blocks, nitems) : nitems);
 #define V(S_, T_)                                                                               \
   case S_:                                                                                      \
-    if (vec_bytes == 16) k_minmax_vec<S_, 16 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows); \
-    else k_minmax_vec<S_, 8 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows);                  \
+    if (vec_bytes == 16) k_minmax_vec<S_, 16 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows, nrb, nitems); \
+    else k_minmax_vec<S_, 8 / sizeof(T_)><<<vgrid, 256, 0, s>>>(a.raster, a.streams, a.norm, rows, nrb, nitems);                  \
     return hipGetLastError();
     switch (src) {
       V(ST_U8, uint8_t) V(ST_I8, int8_t) V(ST_U16, uint16_t) V(ST_I16, int16_t)
