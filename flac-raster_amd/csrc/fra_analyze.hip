@@ -90,13 +90,12 @@ struct AnalyzeSmem {
   // sample i at sidx(i); [0, kSmpStride) = zero chunk.  16-bit path: int16 (every sample fits), which
   // keeps the workgroup at <= 32 KiB LDS (5 workgroups per CU at 96 VGPRs)
   typename std::conditional<B32, int32_t, int16_t>::type smp[kSmpWords];
+  // the encoded subframe (big-endian words, MSB first) is built in smp, dead once the winner's residuals
+  // are in registers (32-bps: <= 40 KiB, 4 workgroups per CU instead of 3; 16-bit: <= 22.75 KiB)
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
-    // encoded subframe (big-endian words, MSB first).  32-bps path: the buffer aliases smp, dead once
-    // the winner's residuals are in registers (keeps the workgroup at <= 40 KiB: 4 per CU, not 3)
-    uint32_t buf[B32 ? 1 : buf_words<B32>()];
   } u;
-  int32_t warm[kMaxLpc];  // 32-bps path: warm-up samples, saved before smp is reused as the bit buffer
+  int32_t warm[kMaxLpc];  // warm-up samples, saved before smp is reused as the bit buffer
   union {
     unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
     struct {  // after the model search (node is dead): winner's exact-pass sums / Rice parameters
@@ -107,8 +106,10 @@ struct AnalyzeSmem {
   } nu;
   double red[kWinCap<MAXLAG>()][4][MAXLAG + 1];  // per window, per wave: reduced chunk partials
   double lp[kWinCap<MAXLAG>()][MAXLAG > 0 ? lp_row(MAXLAG) : 1];  // LD rows per window (triangular)
-  int32_t mcoef[kMaxModels][kMaxLpc];
-  int32_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
+  // model table in the narrowest types (16-bit path: 7 workgroups per CU need <= 22.5 KiB of LDS):
+  // qlp coefficients < 2^15, orders/shifts/partition orders < 128
+  int16_t mcoef[kMaxModels][kMaxLpc];
+  int8_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
   // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
   // partition order (written by porder_search, read by the winner's exact pass)
@@ -223,7 +224,7 @@ __device__ __forceinline__ uint32_t lpc_abs16(const int32_t* x, const int32_t* q
 
 // FRA-1 3.7: the two FIXED orders with the smallest block total of 2|r| (first minimum first; invalid
 // orders skipped) == oracle fg1/fg2.  Wave-uniform, every wave may run it.
-__device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kMaxPart], const int32_t* mvalid, int P,
+__device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kMaxPart], const int8_t* mvalid, int P,
                                              int lane, int& g1, int& g2) {
   uint64_t T[5];
 #pragma unroll
@@ -355,7 +356,7 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 }
 
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 6)) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   const int g = a.frame_base + (int)blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -817,7 +818,7 @@ read_x28(S.smp, t, x);
         for (int jj = 0; jj < 12; jj++)
           if (jj < o) uu[jj] = 0u;
       }
-      if (B32 && t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the next barrier
+      if (t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the next barrier
       // 16-bit: u < 2^28, so 16 of them fit 32 bits; 32-bps: 64-bit partial sums
       typename std::conditional<B32, uint64_t, uint32_t>::type fs0 = 0, fs1 = 0, fs2 = 0;
       {
@@ -903,12 +904,12 @@ read_x28(S.smp, t, x);
       // encode (RFC 9639 9.2) into the LDS bit buffer (over psum: every wave is past its psum reads)
       const uint32_t fbits = verbatim ? verb : (uint32_t)exact;
       const uint32_t nw = (fbits + 31) >> 5;
-      if (B32 && verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
+      if (verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
         verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
         return;
       }
-      // 32-bps: the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
-      uint32_t* buf = B32 ? reinterpret_cast<uint32_t*>(S.smp) : S.u.buf;
+      // the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
+      uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
       for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
       const int pb = big ? 5 : 4;
       const int dk = kcur - k0;
@@ -927,11 +928,8 @@ read_x28(S.smp, t, x);
         lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
         if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
       }
-      if (verbatim) {
-        for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
-      } else {
-        if (t < o)
-          lds_put(buf, hdr + (uint32_t)t * sbps, (uint32_t)(B32 ? S.warm[t] : (int32_t)S.smp[sidx(t)]) & smask, sbps);
+      {
+        if (t < o) lds_put(buf, hdr + (uint32_t)t * sbps, (uint32_t)S.warm[t] & smask, sbps);
         uint32_t pos = hdr + (uint32_t)o * sbps;
         if (type == 3) {
           if (t == 0) {
@@ -1045,7 +1043,7 @@ read_x28(S.smp, t, x);
       uu[jj] = (i < n && i >= o) ? uv : 0u;
     }
   }
-  if (B32 && t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the decision
+  if (t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the decision
   __syncthreads();
   {
     const int pz = n >> ps;
@@ -1149,16 +1147,14 @@ read_x28(S.smp, t, x);
   const uint32_t fbits = S.fbits;
   const uint32_t nw = (fbits + 31) >> 5;
   const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
-  if constexpr (B32) {
-    if (ftype == 1) {
-      // VERBATIM (rare): straight from smp to the slot (the aliased bit buffer is not touched)
-      verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
-      return;
-    }
+  if (ftype == 1) {
+    // VERBATIM (rare): straight from smp to the slot (the aliased bit buffer is not touched)
+    verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+    return;
   }
-  // 32-bps path: every smp read (the winner's residuals, the warm-up copy) precedes the decision barrier
-  uint32_t* buf = B32 ? reinterpret_cast<uint32_t*>(S.smp) : S.u.buf;
-  static_assert(!B32 || sizeof(S.smp) >= sizeof(uint32_t) * (buf_words<true>() + 1), "bit buffer inside smp");
+  // every smp read (the winner's residuals, the warm-up copy) precedes the decision barrier
+  uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
+  static_assert(sizeof(S.smp) >= sizeof(uint32_t) * (buf_words<B32>() + 1), "bit buffer inside smp");
   for (uint32_t j = t; j <= nw; j += kThreads) buf[j] = 0u;
   __syncthreads();
   if (t == 0) {
@@ -1166,12 +1162,9 @@ read_x28(S.smp, t, x);
     lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
     if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
   }
-  if (ftype == 1) {
-    for (int i = t; i < n; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.smp[sidx(i)] & smask, sbps);
-  } else {
+  {
     const int pb = S.fmethod ? 5 : 4;
-    for (int i = t; i < o; i += kThreads)
-      lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)(B32 ? S.warm[i] : (int32_t)S.smp[sidx(i)]) & smask, sbps);
+    for (int i = t; i < o; i += kThreads) lds_put(buf, hdr + (uint32_t)i * sbps, (uint32_t)S.warm[i] & smask, sbps);
     uint32_t pos = hdr + (uint32_t)o * sbps;
     if (ftype == 3) {
       if (t == 0) {
