@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "fra_device.h"
+#include "fra_dw.h"
 
 namespace fra {
 
@@ -337,38 +338,67 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
 // the sample array): word j = the <= 3 samples (sbps >= 16 bits... any sbps >= 1) overlapping bits
 // [32 j, 32 j + 32) of header (8 + w bits) + samples, MSB first -- the words lds_put would produce
 template <typename SmpT>
-__device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t nw,
-                                 int t) {
+__device__ __forceinline__ uint32_t verbatim_word(const SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t j) {
   const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
   const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
-  for (uint32_t j = t; j < nw; j += kThreads) {
-    const int64_t wb = 32 * (int64_t)j;
-    uint32_t word = j == 0 ? (uint32_t)(hv >> 32) : (j == 1 ? (uint32_t)hv : 0u);
-    const int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
-    for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
-      const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
-      const int sft = 32 - (int)rel - sbps;
-      const uint64_t v = (uint64_t)((uint32_t)smp[sidx(s)] & smask);
-      word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
-    }
-    slot[j] = word;
+  const int64_t wb = 32 * (int64_t)j;
+  uint32_t word = j == 0 ? (uint32_t)(hv >> 32) : (j == 1 ? (uint32_t)hv : 0u);
+  const int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
+  for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
+    const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
+    const int sft = 32 - (int)rel - sbps;
+    const uint64_t v = (uint64_t)((uint32_t)smp[sidx(s)] & smask);
+    word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
+  }
+  return word;
+}
+template <typename SmpT>
+__device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t nw,
+                                 int t) {
+  for (uint32_t j = t; j < nw; j += kThreads) slot[j] = verbatim_word(smp, n, hdr, w, sbps, j);
+}
+// direct write: the VERBATIM words into the (aliased) LDS bit buffer -- all computed into registers first
+template <typename SmpT>
+__device__ __forceinline__ void verbatim_to_lds(SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t nw, int t) {
+  constexpr int R = (kMaxBlock / 2 + 16 + kThreads - 1) / kThreads;  // 16-bit: <= 2049 words + 1
+  uint32_t vw[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t j = (uint32_t)(t + r * kThreads);
+    vw[r] = j < nw ? verbatim_word(smp, n, hdr, w, sbps, j) : 0u;
+  }
+  __syncthreads();
+  uint32_t* buf = reinterpret_cast<uint32_t*>(smp);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t j = (uint32_t)(t + r * kThreads);
+    if (j <= nw) buf[j] = vw[r];
   }
 }
 
-template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_analyze(JobArgs a, int src) {
+// DW: direct-write instance (16-bit, no mid-side): 1-D grid of frames x channels in
+// frame-major order, the encoded subframe goes straight to its final place in the output (fra_dw.h)
+template <bool B32, int MAXLAG, bool DW>
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 : 7))) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
+  static_assert(!(DW && B32), "direct write: 16-bit instance only");
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  const int g = a.frame_base + (int)blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int li = (int)blockIdx.x;  // direct write: the launch-relative subframe (frame-major)
+  const int g = a.frame_base + (DW ? li / a.cmax : (int)blockIdx.x);
   // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the
   // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
   // the encoder's scan) keeps the physical wave index wv
-  const int rw = (wv + (int)((blockIdx.x + blockIdx.y) & 3)) & 3;
+  const int rw = (wv + (int)((DW ? (unsigned)li : blockIdx.x + blockIdx.y) & 3)) & 3;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
   // 16-bit instance, M and S (bps + 1 bits) by the 32-bit one, whose grid rows 0-1 are channels 2-3
-  const int c = (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
+  const int c = DW ? li % a.cmax : (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
+  uint32_t dw_len = 0;  // direct write: bits of the encoded subframe left in the LDS bit buffer
+  bool dw_early = true;  // aggregate published + CRC tables copied before the exit (all but CONSTANT)
+  bool dw_sync = false;  // the bit buffer was written after the last barrier (VERBATIM)
+  const uint64_t dw_t0 = DW ? __builtin_amdgcn_s_memrealtime() : 0;
   if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
   const int n = fr.n;
   const int bps = st.bps + ((st.ms && c == 3) ? 1 : 0);
@@ -416,14 +446,21 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_an
       d->type = 0; d->order = 0; d->wasted = 0; d->sbps = (uint8_t)bps; d->cval = vmin;
       d->bits = 8u + (uint32_t)bps; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
       // blob: 8 header bits (type 0, no wasted bits) + the value in bps bits, MSB first
-      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+      uint32_t* slot = DW ? reinterpret_cast<uint32_t*>(S.smp) : a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
       const uint64_t v = (uint64_t)(uint32_t)vmin & (bps >= 32 ? 0xFFFFFFFFull : ((1ull << bps) - 1));
       const uint64_t blob = v << (64 - 8 - bps);  // 8 zero header bits first
       slot[0] = (uint32_t)(blob >> 32);
       slot[1] = (uint32_t)blob;
+      if (DW) slot[2] = 0u;
+    }
+    if constexpr (DW) {
+      dw_len = 8u + (uint32_t)bps;
+      dw_early = false;
+      goto dw_tail;
     }
     return;
   }
+  {  // (direct write: every exit below leaves through dw_tail)
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
   if (w) {
@@ -865,6 +902,7 @@ read_x28(S.smp, t, x);
       }
       __syncthreads();
       FRA_STOP(6)
+      if constexpr (DW) dw_tables(a, *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t);  // (psum is dead)
       // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
       const int npp = 1 << ps;
       const int k0j = lane < npp ? (int)S.kbest[m][lane] : 0;
@@ -903,10 +941,20 @@ read_x28(S.smp, t, x);
       }
       // encode (RFC 9639 9.2) into the LDS bit buffer (over psum: every wave is past its psum reads)
       const uint32_t fbits = verbatim ? verb : (uint32_t)exact;
+      if constexpr (DW) {
+        if (t == 0) dw_publish(a, li, fbits);
+      }
       const uint32_t nw = (fbits + 31) >> 5;
       if (verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
-        verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
-        return;
+        if constexpr (DW) {
+          verbatim_to_lds(S.smp, n, hdr, w, sbps, nw, t);
+          dw_len = verb;
+          dw_sync = true;
+          goto dw_tail;
+        } else {
+          verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+          return;
+        }
       }
       // the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
       uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
@@ -957,9 +1005,14 @@ read_x28(S.smp, t, x);
         }
       }
       __syncthreads();
-      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
-      for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
-      return;
+      if constexpr (DW) {
+        dw_len = fbits;
+        goto dw_tail;
+      } else {
+        uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+        for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+        return;
+      }
     }
   }
   if (rw == 0) {  // winner = first minimal estimate: argmin over (estimate, model index)
@@ -1145,12 +1198,23 @@ read_x28(S.smp, t, x);
   // ---- 7. encode the subframe (RFC 9639 9.2) into the LDS bit buffer and store it to its slot
   const int ftype = S.ftype;
   const uint32_t fbits = S.fbits;
+  if constexpr (DW) {  // (esum over psum is dead since the decision)
+    dw_tables(a, *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t);
+    if (t == 0) dw_publish(a, li, fbits);
+  }
   const uint32_t nw = (fbits + 31) >> 5;
   const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
   if (ftype == 1) {
     // VERBATIM (rare): straight from smp to the slot (the aliased bit buffer is not touched)
-    verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
-    return;
+    if constexpr (DW) {
+      verbatim_to_lds(S.smp, n, hdr, w, sbps, nw, t);
+      dw_len = fbits;
+      dw_sync = true;
+      goto dw_tail;
+    } else {
+      verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+      return;
+    }
   }
   // every smp read (the winner's residuals, the warm-up copy) precedes the decision barrier
   uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
@@ -1240,16 +1304,42 @@ read_x28(S.smp, t, x);
     }
   }
   __syncthreads();
-  uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
-  for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+  if constexpr (DW) {
+    dw_len = fbits;
+  } else {
+    uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+    for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+  }
+  }  // (direct-write block)
+dw_tail:
+  if constexpr (DW) {
+    dw_emit(a, reinterpret_cast<const uint32_t*>(S.smp), dw_len, li, a.cmax, dw_t0,
+            *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t, dw_early, dw_sync);
+  }
 }
 
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s) {
+// the diagnostic phase-stop builds return early from k_analyze: no direct write there
+bool analyze_dw_capable() {
+#ifdef FRA_DIAG_STOP
+  return false;
+#else
+  return true;
+#endif
+}
+
+hipError_t launch_analyze(int src, bool b32, bool ms, bool dw, const JobArgs& a, hipStream_t s) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
+  if (dw && !b32 && !ms) {  // direct write: frame-major 1-D grid (launch order = output order)
+    const dim3 g1((unsigned)((int64_t)a.frame_count * a.cmax));
+    if (ml == 0) k_analyze<false, 0, true><<<g1, kThreads, 0, s>>>(a, src);
+    else if (ml == 8) k_analyze<false, 8, true><<<g1, kThreads, 0, s>>>(a, src);
+    else k_analyze<false, 12, true><<<g1, kThreads, 0, s>>>(a, src);
+    return hipGetLastError();
+  }
+#define FRA_LAUNCH(B, M) k_analyze<B, M, false><<<grid, kThreads, 0, s>>>(a, src)
   if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
     grid.y = 2;

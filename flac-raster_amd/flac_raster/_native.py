@@ -90,6 +90,7 @@ EXPORTS = [
     "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d", "fra_plan_frame_offsets", "fra_normalize",
     "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
     "fra_host_register", "fra_host_unregister", "fra_tiff_decode", "fra_plan_set_first_frame",
+    "fra_plan_flags",
 ]
 
 
@@ -139,6 +140,7 @@ def load():
         L.fra_plan_encode_host.argtypes = [vp, vp, vp, u64, C.POINTER(u64)]
         L.fra_plan_capacity.argtypes = [vp, C.POINTER(u64), C.POINTER(i32)]
         L.fra_plan_set_first_frame.argtypes = [vp, i32]
+        L.fra_plan_flags.argtypes = [vp, C.POINTER(i32)]
         L.fra_host_alloc.argtypes = [u64, C.POINTER(vp)]
         L.fra_host_free.argtypes = [vp]
         L.fra_host_register.argtypes = [vp, u64]
@@ -361,6 +363,12 @@ class Plan:
     def set_first_frame(self, n: int):
         """FLAC frame number of every stream's first frame for the next execute (pyflac shim)."""
         _check(load().fra_plan_set_first_frame(self.h, int(n)))
+
+    def flags(self) -> int:
+        """``FRA_PLAN_*`` bits: 1 direct write (subframes placed by k_analyze), 2 cross-execute pipelined."""
+        f = C.c_int32()
+        _check(load().fra_plan_flags(self.h, C.byref(f)))
+        return f.value
 
     def capacity(self) -> Tuple[int, int]:
         """(upper bound of the output bytes, number of host-pipeline row bands)."""
