@@ -12,4 +12,7 @@ timeout -k 10 200 python -u bench.py --no-cpu --no-e2e --no-pmc > $OUT/bench.jso
 python -c "import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'])"
 FRA_DW=1 timeout -k 10 200 python -u bench.py --no-cpu --no-e2e --no-pmc > $OUT/bench_dw.json 2> $OUT/bench_dw.err || { echo BENCH_FAILED; exit 1; }
 python -c "import json; d=json.loads(open('$OUT/bench_dw.json').read().strip().splitlines()[-1]); print('dw', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'])"
+
+FRA_ASM_WG=4 timeout -k 10 200 python -u bench.py --no-cpu --no-e2e --no-pmc > $OUT/bench_asm4.json 2> $OUT/bench_asm4.err || { echo BENCH_FAILED; exit 1; }
+python -c "import json; d=json.loads(open('$OUT/bench_asm4.json').read().strip().splitlines()[-1]); print('asm4', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'])"
 echo ALLOK
