@@ -383,7 +383,9 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   static_assert(!(DW && B32), "direct write: 16-bit instance only");
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
+  // 7-wave 16-bit instance (the direct-write instance keeps its measured, spill-free allocation)
+  const int t = threadIdx.x, lane = t & 63, wv = DW ? (t >> 6) : __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = (int)blockIdx.x;  // direct write: the launch-relative subframe (frame-major)
   const int g = a.frame_base + (DW ? li / a.cmax : (int)blockIdx.x);
   // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the

@@ -15,7 +15,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libflac_raster_amd.so"
+# FRA_LIB_PATH: load another build of the library (same-box A/B experiments, tools/gpu_ab.sh)
+_LIB_PATH = Path(os.environ.get("FRA_LIB_PATH") or Path(__file__).resolve().parent / "_lib" / "libflac_raster_amd.so")
 _lib = None
 _lock = threading.Lock()
 
