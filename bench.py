@@ -215,13 +215,17 @@ def _med(v):
 
 
 def inrun_pmc(args, kernel):
-    """HBM traffic (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction; KiB) and VALU
-    instruction counts of ``kernel``'s median launch, from separate passes."""
+    """HBM traffic (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction; KiB), VALU
+    instruction counts and the wave-cycle split of ``kernel``'s median launch, from separate passes.
+    SQ_WAVE_CYCLES = SQ_WAIT_ANY (parked at s_waitcnt / s_barrier) + SQ_WAIT_INST_ANY (ready, not issued)
+    + SQ_ACTIVE_INST_ANY (issuing), all in quad-cycles (MI355X_MICROARCH.md "rocprofv3 PMC slots")."""
     res = {"source": "in-run rocprofv3 --pmc passes of this build (bench.py --child, 1 step)"}
     fe = pmc_pass(args, ["FETCH_SIZE"], "fetch")
     wr = pmc_pass(args, ["WRITE_SIZE"], "write")
-    va = pmc_pass(args, ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"], "valu")
-    gr = pmc_pass(args, ["GRBM_GUI_ACTIVE"], "grbm")
+    va = pmc_pass(args, ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                         "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"], "valu")
+    gr = pmc_pass(args, ["SQ_WAVES", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT",
+                         "GRBM_GUI_ACTIVE"], "grbm")
     if fe and wr and kernel in fe and kernel in wr:
         res["traffic"] = int(2 * _med(fe[kernel]["FETCH_SIZE"]) * 1024 + _med(wr[kernel]["WRITE_SIZE"]) * 1024)
         res["traffic_by_kernel"] = {k: int(2 * _med(fe[k].get("FETCH_SIZE")) * 1024 +
@@ -233,10 +237,74 @@ def inrun_pmc(args, kernel):
         res["valu_insts"] = int(_med(v.get("SQ_INSTS_VALU")))
         res["valu_per_wave"] = round(res["valu_insts"] / waves, 1) if waves else None
         res["salu_per_wave"] = round(_med(v.get("SQ_INSTS_SALU")) / waves, 1) if waves else None
-        res["lds_per_wave"] = round(_med(v.get("SQ_INSTS_LDS")) / waves, 1) if waves else None
+        wc = _med(v.get("SQ_WAVE_CYCLES"))
+        if wc:
+            st = {"wave_quad_cycles_per_wave": round(wc / waves, 1),
+                  "parked_waitcnt_or_barrier": round(_med(v.get("SQ_WAIT_ANY")) / wc, 4),
+                  "ready_not_issued": round(_med(v.get("SQ_WAIT_INST_ANY")) / wc, 4),
+                  "issuing": round(_med(v.get("SQ_ACTIVE_INST_ANY")) / wc, 4),
+                  "issuing_valu": round(_med(v.get("SQ_ACTIVE_INST_VALU")) / wc, 4)}
+            st["dominant"] = max(("parked_waitcnt_or_barrier", "ready_not_issued", "issuing"), key=lambda k: st[k])
+            res["stalls"] = st
     if gr and kernel in gr:
-        res["busy_cycles_per_xcd"] = int(_med(gr[kernel].get("GRBM_GUI_ACTIVE")) / XCDS)
+        g = gr[kernel]
+        res["busy_cycles_per_xcd"] = int(_med(g.get("GRBM_GUI_ACTIVE")) / XCDS)
+        waves = _med(g.get("SQ_WAVES"))
+        if waves:
+            res["lds_per_wave"] = round(_med(g.get("SQ_INSTS_LDS")) / waves, 1)
+            res["lds_issue_stall_quad_cycles_per_wave"] = round(_med(g.get("SQ_WAIT_INST_LDS")) / waves, 1)
+            res["lds_bank_conflict_cycles_per_wave"] = round(_med(g.get("SQ_LDS_BANK_CONFLICT")) / waves, 1)
     return res
+
+
+def inrun_kernel_stats(args, out_dir):
+    """rocprofv3 --kernel-trace --stats over a child run that executes ONLY the plan (``--child``: the
+    warmup + timed executes of this config, no parity launches, no CPU / e2e legs) in the roofline's serial
+    timing mode (each kernel alone, as the HIP events of ``roofline.achieved`` measure it), so the
+    per-kernel averages are those launches.  The stats CSV is copied to ``out_dir`` (tagged with the
+    kernel-source hash); returns {kernel: {calls, avg_ms, min_ms, max_ms}}."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    tmp = tempfile.mkdtemp(prefix="fra_kt_", dir="/tmp")
+    cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp, "-o", "run", "--",
+           sys.executable, str(ROOT / "bench.py"), "--config", args.config, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--child", "--child-serial"]
+    if args.level is not None:
+        cmd += ["--level", str(args.level)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=float(os.environ.get("FRA_PMC_TIMEOUT", "150")), check=True)
+    except (subprocess.SubprocessError, OSError):
+        shutil.rmtree(tmp, ignore_errors=True)
+        return None
+    f = next(Path(tmp).rglob("*kernel_stats.csv"), None)
+    out = {}
+    if f is not None:
+        for r in csv.DictReader(open(f)):
+            out[_short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": round(float(r["AverageNs"]) / 1e6, 5),
+                                     "min_ms": round(float(r["MinNs"]) / 1e6, 5),
+                                     "max_ms": round(float(r["MaxNs"]) / 1e6, 5)}
+        if out_dir:
+            try:
+                Path(out_dir).mkdir(parents=True, exist_ok=True)
+                shutil.copy(f, Path(out_dir) / f"{args.config}_n1_{sources_sha()}_timed_kernel_stats.csv")
+            except OSError:
+                pass
+    shutil.rmtree(tmp, ignore_errors=True)
+    return out or None
+
+
+def reference_cpu_probe():
+    """the reference's own CPU path is pyflac (libFLAC 1.4.3) or the ``flac`` CLI on
+    the node.  Probed, never installed; absent here, so the CPU baseline stays the oracle port."""
+    import importlib.util
+    pyflac = importlib.util.find_spec("pyflac") is not None
+    cli = shutil.which("flac")
+    return {"pyflac_importable": pyflac, "flac_cli": cli, "libflac_on_node": bool(pyflac or cli)}
 
 
 def committed_profile(args, cfg, kernel):
@@ -269,7 +337,11 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
+    ap.add_argument("--no-trace", action="store_true", help="skip the in-run rocprofv3 kernel-trace pass")
+    ap.add_argument("--prof-dir", default=os.environ.get("FRA_PROF_DIR", str(ROOT / "gpurun_out" / "bench_prof")),
+                    help="where the timed-launch kernel-stats CSV of the in-run trace pass is copied")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)  # PMC child: steps only
+    ap.add_argument("--child-serial", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-mp-child", nargs=2, type=int, metavar=("PROCS", "TILES"), help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_mp_child:
@@ -323,6 +395,8 @@ def main():
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
 
     if args.child:  # rocprofv3 child: the plan's launches only
+        if args.child_serial:  # the roofline's mode: serial executes, each kernel alone on the device
+            plan.enable_timing(True)
         for _ in range(args.warmup + args.steps):
             plan.execute()
         plan.sync()
@@ -431,6 +505,9 @@ def main():
         plan.close()
         ctx.free(dev_raster)
         plan = dev_raster = None
+        kstats = None
+        if not args.no_trace and world == 1:
+            kstats = inrun_kernel_stats(args, args.prof_dir)
         pm = None
         if not args.no_pmc and world == 1:
             pm = inrun_pmc(args, dom_name)
@@ -481,6 +558,12 @@ def main():
                          "counters": pm,
                          "valu_note": f"valu_issue_frac = SQ_INSTS_VALU x {VALU_CYC} cyc / ({SIMDS} SIMDs x "
                                       "GRBM_GUI_ACTIVE/8) of the same launch"},
+            "kernel_stats": ({"source": "rocprofv3 --kernel-trace --stats over bench.py --child --child-serial "
+                                        f"(the plan's {args.warmup}+{args.steps} executes only, serial as the "
+                                        "roofline's HIP events, no parity launches), CSV "
+                                        f"{args.config}_n1_{sources_sha()}_timed_kernel_stats.csv",
+                              "sources_sha": sources_sha(), "kernels": kstats} if kstats else None),
+            "reference_cpu": reference_cpu_probe(),
             "cpu_baseline": cpu,
             "cpu_baseline_mp": cpu_mp,
             "size_ratio_vs_libflac_c2": size_c2,

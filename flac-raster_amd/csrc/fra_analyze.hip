@@ -24,10 +24,34 @@
 //      over k-1..k+1; VERBATIM if not smaller
 #include <type_traits>
 
+#if defined(FRA_STAMPS) && defined(FRA_STAMPS_FINE)
+// finer load-phase stamps: thread 0 after the value `dep` has arrived (the data dependency orders the
+// stamp after the load it depends on)
+namespace fra { extern __device__ unsigned long long g_fra_stamps[]; }
+#define FRA_LOAD_STAMP(k, dep)                                                                       \
+  if (threadIdx.x == 0 && (dep) != 0x7FFFFFF1) {                                                     \
+    const unsigned wgi_ = blockIdx.x * gridDim.y + blockIdx.y;                                       \
+    if (wgi_ < (1u << 17)) g_fra_stamps[wgi_ * 16u + (k)] = __builtin_amdgcn_s_memtime();            \
+  }
+#endif
 #include "fra_device.h"
-#include "fra_dw.h"
 
 namespace fra {
+
+#ifdef FRA_STAMPS
+// diagnostic build only (csrc/Makefile `stamps`, tools/stamp_phases.py): wave 0 of the first kStampWG
+// workgroups stores s_memtime after each phase barrier, so phase durations are measured inside the
+// real, mixed steady state (every other workgroup keeps running the full kernel)
+constexpr unsigned kStampWG = 1u << 17, kStampN = 16;
+__device__ unsigned long long g_fra_stamps[kStampWG * kStampN];
+#define FRA_STAMP(k)                                                                          \
+  if (threadIdx.x == 0) {                                                                      \
+    const unsigned wgi_ = blockIdx.x * gridDim.y + blockIdx.y;                                 \
+    if (wgi_ < kStampWG) g_fra_stamps[wgi_ * kStampN + (k)] = __builtin_amdgcn_s_memtime();   \
+  }
+#else
+#define FRA_STAMP(k)
+#endif
 
 // encoded-subframe buffer: >= (max subframe bits + 31) / 32 + 1 words (VERBATIM bound)
 template <bool B32>
@@ -79,6 +103,21 @@ __device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)
     const uint32_t v = d[(t + 2) * kSmpStride / 2 + j];
     y[16 + 2 * j] = lo16(v);
     y[17 + 2 * j] = hi16(v);
+  }
+}
+
+// apodization coefficients of samples i0 .. i0 + 16 + MAXLAG - 1 of one window (row of the plan's window
+// table, exactly n entries used): unconditional vector loads when the whole span lies inside the block,
+// else only the entries below n (the others are never multiplied: wf = 0 past n) -- no read past the
+// window the frame owns (the table is allocated at its exact size)
+template <int MAXLAG>
+__device__ __forceinline__ void load_window(const float* win, int i0, int n, float (&w)[kChunk + MAXLAG]) {
+  if (i0 + kChunk + MAXLAG <= n) {
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = win[i0 + j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = i0 + j < n ? win[i0 + j] : 0.0f;
   }
 }
 
@@ -357,50 +396,24 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
                                  int t) {
   for (uint32_t j = t; j < nw; j += kThreads) slot[j] = verbatim_word(smp, n, hdr, w, sbps, j);
 }
-// direct write: the VERBATIM words into the (aliased) LDS bit buffer -- all computed into registers first
-template <typename SmpT>
-__device__ __forceinline__ void verbatim_to_lds(SmpT* smp, int n, uint32_t hdr, int w, int sbps, uint32_t nw, int t) {
-  constexpr int R = (kMaxBlock / 2 + 16 + kThreads - 1) / kThreads;  // 16-bit: <= 2049 words + 1
-  uint32_t vw[R];
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const uint32_t j = (uint32_t)(t + r * kThreads);
-    vw[r] = j < nw ? verbatim_word(smp, n, hdr, w, sbps, j) : 0u;
-  }
-  __syncthreads();
-  uint32_t* buf = reinterpret_cast<uint32_t*>(smp);
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const uint32_t j = (uint32_t)(t + r * kThreads);
-    if (j <= nw) buf[j] = vw[r];
-  }
-}
-
-// DW: direct-write instance (16-bit, no mid-side): 1-D grid of frames x channels in
-// frame-major order, the encoded subframe goes straight to its final place in the output (fra_dw.h)
-template <bool B32, int MAXLAG, bool DW>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 : 7))) k_analyze(JobArgs a, int src) {
+template <bool B32, int MAXLAG>
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
-  static_assert(!(DW && B32), "direct write: 16-bit instance only");
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
-  // 7-wave 16-bit instance (the direct-write instance keeps its measured, spill-free allocation)
-  const int t = threadIdx.x, lane = t & 63, wv = DW ? (t >> 6) : __builtin_amdgcn_readfirstlane(t >> 6);
-  const int li = (int)blockIdx.x;  // direct write: the launch-relative subframe (frame-major)
-  const int g = a.frame_base + (DW ? li / a.cmax : (int)blockIdx.x);
+  // 7-wave 16-bit instance
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = a.frame_base + (int)blockIdx.x;
   // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the
   // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
   // the encoder's scan) keeps the physical wave index wv
-  const int rw = (wv + (int)((DW ? (unsigned)li : blockIdx.x + blockIdx.y) & 3)) & 3;
+  const int rw = (wv + (int)((blockIdx.x + blockIdx.y) & 3)) & 3;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
   // 16-bit instance, M and S (bps + 1 bits) by the 32-bit one, whose grid rows 0-1 are channels 2-3
-  const int c = DW ? li % a.cmax : (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
-  uint32_t dw_len = 0;  // direct write: bits of the encoded subframe left in the LDS bit buffer
-  bool dw_early = true;  // aggregate published + CRC tables copied before the exit (all but CONSTANT)
-  bool dw_sync = false;  // the bit buffer was written after the last barrier (VERBATIM)
-  const uint64_t dw_t0 = DW ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int c = (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
+  FRA_STAMP(0)
   if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
   const int n = fr.n;
   const int bps = st.bps + ((st.ms && c == 3) ? 1 : 0);
@@ -425,6 +438,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
   {
     const NormParams np = norm_params(st, a.norm[fr.stream]);
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
+    FRA_LOAD_STAMP(11, (int)np.mn + st.width + fr.n)
     load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
@@ -433,10 +447,12 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys
   const uint32_t kmax = ~wave_min32(~((uint32_t)vmax ^ 0x80000000u));
   if (lane == 0) { S.ired[wv][0] = orv; S.ired[wv][1] = kmin; S.ired[wv][2] = kmax; }
+  FRA_LOAD_STAMP(14, (int)kmax)
   __syncthreads();
   orv = S.ired[0][0] | S.ired[1][0] | S.ired[2][0] | S.ired[3][0];
   vmin = (int32_t)(min(min(S.ired[0][1], S.ired[1][1]), min(S.ired[2][1], S.ired[3][1])) ^ 0x80000000u);
   vmax = (int32_t)(max(max(S.ired[0][2], S.ired[1][2]), max(S.ired[2][2], S.ired[3][2])) ^ 0x80000000u);
+  FRA_STAMP(1)
 
   FRA_STOP(1)
   // ---- 2. CONSTANT / wasted bits (3.2, 3.3)
@@ -448,21 +464,15 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
       d->type = 0; d->order = 0; d->wasted = 0; d->sbps = (uint8_t)bps; d->cval = vmin;
       d->bits = 8u + (uint32_t)bps; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
       // blob: 8 header bits (type 0, no wasted bits) + the value in bps bits, MSB first
-      uint32_t* slot = DW ? reinterpret_cast<uint32_t*>(S.smp) : a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+      uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
       const uint64_t v = (uint64_t)(uint32_t)vmin & (bps >= 32 ? 0xFFFFFFFFull : ((1ull << bps) - 1));
       const uint64_t blob = v << (64 - 8 - bps);  // 8 zero header bits first
       slot[0] = (uint32_t)(blob >> 32);
       slot[1] = (uint32_t)blob;
-      if (DW) slot[2] = 0u;
-    }
-    if constexpr (DW) {
-      dw_len = 8u + (uint32_t)bps;
-      dw_early = false;
-      goto dw_tail;
     }
     return;
   }
-  {  // (direct write: every exit below leaves through dw_tail)
+  {
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
   if (w) {
@@ -530,6 +540,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
     }
   }
   FRA_STOP(9)
+  FRA_STAMP(2)
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = fixfast && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
@@ -538,8 +549,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
   float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
   if constexpr (MAXLAG > 0) {
     const float* win = a.win + (size_t)fr.win * a.nwin * a.blocksize;
-#pragma unroll
-    for (int j = 0; j < kChunk + MAXLAG; j++) wcur[j] = win[t * kChunk + j];  // table padded by kMaxLpc
+    load_window<MAXLAG>(win, t * kChunk, n, wcur);
   }
   // partial windows are zero outside their segment (host-computed extent [lo, hi)): a wave whose
   // samples + lookahead [1024 wv, 1024 wv + 1024 + MAXLAG) miss it would only sum exact products of
@@ -600,13 +610,11 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
         float wl[kChunk + MAXLAG];
         const bool act = wave_active(wi);
         const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
-        if (act) {
-#pragma unroll
-          for (int j = 0; j < kChunk + MAXLAG; j++) wl[j] = win[i0 + j];  // table padded by kMaxLpc
-        }
+        if (act) load_window<MAXLAG>(win, i0, n, wl);
         window_acf(wi, wl, act);
       }
       __syncthreads();
+      FRA_STAMP(3)
       FRA_STOP(8)
       // Levinson-Durbin, order choice and quantisation of 4 windows per wave at once: window wi on wave
       // wi / 4, lanes 16 (wi % 4) .. +15 (the same op sequence per lane: one window's instruction cost for
@@ -689,6 +697,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : (DW ? 6 
 read_x28(S.smp, t, x);
   }
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
+  FRA_STAMP(4)
   double xd[B32 ? 12 + kChunk : 1];  // 32-bps fast path: x as exact doubles
   if (fastframe) {
     if constexpr (B32) {
@@ -769,6 +778,7 @@ read_x28(S.smp, t, x);
     }
   }
   __syncthreads();
+  FRA_STAMP(5)
 
   FRA_STOP(3)
   // ---- 5. every partition order of a model in one pass (one wave per model)
@@ -796,6 +806,7 @@ read_x28(S.smp, t, x);
     for (int i = rw * 2 * kMaxPart + lane; i < e1; i += 64) ez[i] = 0ull;
   }
   __syncthreads();
+  FRA_STAMP(6)
   FRA_STOP(5)
   {
     if (fastframe) {
@@ -903,8 +914,8 @@ read_x28(S.smp, t, x);
         atomicAdd(&S.nu.e.esum2[pidx][2], (unsigned long long)fs2);
       }
       __syncthreads();
+      FRA_STAMP(7)
       FRA_STOP(6)
-      if constexpr (DW) dw_tables(a, *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t);  // (psum is dead)
       // exact Rice bits with k refined over k0-1..k0+1 (3.9), lane j = partition j, in every wave
       const int npp = 1 << ps;
       const int k0j = lane < npp ? (int)S.kbest[m][lane] : 0;
@@ -943,20 +954,10 @@ read_x28(S.smp, t, x);
       }
       // encode (RFC 9639 9.2) into the LDS bit buffer (over psum: every wave is past its psum reads)
       const uint32_t fbits = verbatim ? verb : (uint32_t)exact;
-      if constexpr (DW) {
-        if (t == 0) dw_publish(a, li, fbits);
-      }
       const uint32_t nw = (fbits + 31) >> 5;
       if (verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
-        if constexpr (DW) {
-          verbatim_to_lds(S.smp, n, hdr, w, sbps, nw, t);
-          dw_len = verb;
-          dw_sync = true;
-          goto dw_tail;
-        } else {
-          verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
-          return;
-        }
+        verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+        return;
       }
       // the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
       uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
@@ -971,6 +972,7 @@ read_x28(S.smp, t, x);
       const uint32_t inc = wave_incl_scan32(tot);
       if (lane == 63) S.scan[wv] = inc;
       __syncthreads();
+      FRA_STAMP(8)
       FRA_STOP(7)
       const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
       if (t == 0) {
@@ -1007,12 +1009,11 @@ read_x28(S.smp, t, x);
         }
       }
       __syncthreads();
-      if constexpr (DW) {
-        dw_len = fbits;
-        goto dw_tail;
-      } else {
+      FRA_STAMP(9)
+      {
         uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
         for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+        FRA_STAMP(10)
         return;
       }
     }
@@ -1200,23 +1201,12 @@ read_x28(S.smp, t, x);
   // ---- 7. encode the subframe (RFC 9639 9.2) into the LDS bit buffer and store it to its slot
   const int ftype = S.ftype;
   const uint32_t fbits = S.fbits;
-  if constexpr (DW) {  // (esum over psum is dead since the decision)
-    dw_tables(a, *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t);
-    if (t == 0) dw_publish(a, li, fbits);
-  }
   const uint32_t nw = (fbits + 31) >> 5;
   const uint32_t smask = sbps >= 32 ? 0xFFFFFFFFu : ((1u << sbps) - 1u);
   if (ftype == 1) {
     // VERBATIM (rare): straight from smp to the slot (the aliased bit buffer is not touched)
-    if constexpr (DW) {
-      verbatim_to_lds(S.smp, n, hdr, w, sbps, nw, t);
-      dw_len = fbits;
-      dw_sync = true;
-      goto dw_tail;
-    } else {
-      verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
-      return;
-    }
+    verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+    return;
   }
   // every smp read (the winner's residuals, the warm-up copy) precedes the decision barrier
   uint32_t* buf = reinterpret_cast<uint32_t*>(S.smp);
@@ -1306,42 +1296,31 @@ read_x28(S.smp, t, x);
     }
   }
   __syncthreads();
-  if constexpr (DW) {
-    dw_len = fbits;
-  } else {
-    uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
-    for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
-  }
-  }  // (direct-write block)
-dw_tail:
-  if constexpr (DW) {
-    dw_emit(a, reinterpret_cast<const uint32_t*>(S.smp), dw_len, li, a.cmax, dw_t0,
-            *reinterpret_cast<DwScratch*>(&S.u.psum[0][0]), t, dw_early, dw_sync);
+  uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+  for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
   }
 }
 
-// the diagnostic phase-stop builds return early from k_analyze: no direct write there
-bool analyze_dw_capable() {
-#ifdef FRA_DIAG_STOP
-  return false;
-#else
-  return true;
+#ifdef FRA_STAMPS
+}  // namespace fra
+extern "C" __attribute__((visibility("default"))) int fra_diag_stamps(void* host, unsigned long long bytes) {
+  if (!host) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fra::g_fra_stamps)) != hipSuccess) return -1;
+    return hipMemset(d, 0, sizeof(fra::g_fra_stamps)) == hipSuccess ? 0 : -1;
+  }
+  const size_t nb = bytes < sizeof(fra::g_fra_stamps) ? bytes : sizeof(fra::g_fra_stamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(fra::g_fra_stamps), nb, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+namespace fra {
 #endif
-}
 
-hipError_t launch_analyze(int src, bool b32, bool ms, bool dw, const JobArgs& a, hipStream_t s) {
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-  if (dw && !b32 && !ms) {  // direct write: frame-major 1-D grid (launch order = output order)
-    const dim3 g1((unsigned)((int64_t)a.frame_count * a.cmax));
-    if (ml == 0) k_analyze<false, 0, true><<<g1, kThreads, 0, s>>>(a, src);
-    else if (ml == 8) k_analyze<false, 8, true><<<g1, kThreads, 0, s>>>(a, src);
-    else k_analyze<false, 12, true><<<g1, kThreads, 0, s>>>(a, src);
-    return hipGetLastError();
-  }
-#define FRA_LAUNCH(B, M) k_analyze<B, M, false><<<grid, kThreads, 0, s>>>(a, src)
+#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
   if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
     grid.y = 2;

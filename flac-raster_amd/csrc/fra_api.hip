@@ -8,8 +8,6 @@
 //   k_analyze  [frames x channels]
 //   k_frame_bytes + hipcub exclusive scan + k_group_offsets
 //   k_assemble [frames]
-// or, for direct-write plans (16-bit, no mid-side, one frame group: fra_dw.h), only
-//   k_analyze  [frames * channels, frame-major]  (subframes straight to their place, CRC-16, offsets)
 // Large plans run as FRA_GROUPS frame groups on their own streams (fra_plan_execute).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -33,10 +31,7 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
                          hipStream_t s, int max_blocks);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
-hipError_t launch_analyze(int src, bool b32, bool ms, bool dw, const JobArgs& a, hipStream_t s);
-hipError_t launch_frame_headers(const StreamDev* streams, const FrameDev* frames, int nframes, uint32_t* hdr,
-                                uint8_t* hbytes, hipStream_t s);
-bool analyze_dw_capable();
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
@@ -147,6 +142,7 @@ struct fra_plan {
   hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
   bool ana_pending[2] = {false, false};
   bool raster_dirty = false;  // a host raster copy on the plan's stream the norm stream must wait for
+  bool resync = false;        // serial work was queued on the plan's stream since the last pipelined execute
   // timing
   bool timing = false;
   hipEvent_t ev[5] = {};
@@ -154,19 +150,6 @@ struct fra_plan {
   int nexec = 0;
   bool pending_times = false;
   bool executed = false;
-  // direct write (fra_dw.h): look-back words, static frame headers, abort flag (device + page-locked)
-  bool dw = false;
-  DwCtl* d_dwctl = nullptr;
-  DwCtl hdw{};
-  unsigned long long* d_lb = nullptr;
-  size_t lb_bytes = 0;
-  uint32_t* d_hdr = nullptr;
-  uint8_t* d_hbytes = nullptr;
-  int* d_abort = nullptr;
-  int* h_abort = nullptr;
-  unsigned long long* d_dwdiag = nullptr;
-  unsigned long long* d_dwtrace = nullptr;
-  uint32_t epoch = 0;
 };
 
 // ----------------------------------------------------------------------------- host helpers
@@ -222,7 +205,7 @@ static uint32_t gf16_mul(uint32_t a, uint32_t b) {
   return r & 0xFFFFu;
 }
 static std::vector<uint16_t> crc16_tables() {
-  std::vector<uint16_t> tab(kXpowOff + kXOrd);
+  std::vector<uint16_t> tab(kCrcT16Off + 16 * 256);
   for (int v = 0; v < 256; v++) {
     uint32_t d = (uint32_t)v << 8;
     for (int b = 0; b < 8; b++) d = (d & 0x8000u) ? ((d << 1) ^ 0x8005u) : (d << 1);
@@ -246,12 +229,6 @@ static std::vector<uint16_t> crc16_tables() {
       tab[1024 + i * 512 + 256 + b] = (uint16_t)gf16_mul(gf16_mul((uint32_t)b, 0x100), X);
     }
     X = gf16_mul(X, X);
-  }
-  uint32_t xe = 1;  // x^e mod P (direct write: CRC-16 of bit strings at any offset)
-  for (int e = 0; e < kXOrd; e++) {
-    tab[kXpowOff + e] = (uint16_t)xe;
-    xe <<= 1;
-    if (xe & 0x10000u) xe ^= 0x18005u;
   }
   return tab;
 }
@@ -310,22 +287,6 @@ void fra_ctx_destroy(fra_ctx* c) {
 void fra_plan_destroy(fra_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
-  (void)hipFree(p->d_lb);
-  (void)hipFree(p->d_hdr);
-  (void)hipFree(p->d_hbytes);
-  (void)hipFree(p->d_abort);
-  (void)hipFree(p->d_dwctl);
-  if (p->d_dwtrace) {  // FRA_DW_TRACE=path: per-subframe stamps of the last direct-write launch
-    std::vector<unsigned long long> tr(4 * p->frames.size() * p->cmax);
-    if (hipMemcpy(tr.data(), p->d_dwtrace, tr.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
-      if (FILE* f = fopen(getenv("FRA_DW_TRACE"), "ab")) {
-        fwrite(tr.data(), 8, tr.size(), f);
-        fclose(f);
-      }
-    (void)hipFree(p->d_dwtrace);
-  }
-  (void)hipFree(p->d_dwdiag);
-  if (p->h_abort) (void)hipHostFree(p->h_abort);
   (void)hipFree(p->d_raster_owned);
   (void)hipFree(p->d_streams);
   (void)hipFree(p->d_frames);
@@ -553,8 +514,8 @@ static int plan_build(fra_plan* p) {
   HIPCHK(hipMalloc(&p->d_foff, sizeof(unsigned long long) * (nfr + 1)));
   HIPCHK(hipMalloc(&p->d_out, p->out_cap));
   const size_t wn = (size_t)std::max<size_t>(1, win_sizes.size()) * std::max(1, p->nwin) * j.blocksize;
-  // + pad: k_analyze threads read win[16 t + j], j < 16 + max lag, for every t < 256 whatever the block size
-  std::vector<float> wt(wn + kMaxBlock + kMaxLpc, 0.0f);
+  // exact size: k_analyze reads entries [0, n) of the table of block size n only (load_window)
+  std::vector<float> wt(wn, 0.0f);
   for (size_t t = 0; t < win_sizes.size(); t++)
     window_set(wt.data() + t * std::max(1, p->nwin) * j.blocksize, win_sizes[t], j.blocksize, nsub);
   HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wt.size()));
@@ -707,40 +668,6 @@ static int plan_build(fra_plan* p) {
       }
     }
   }
-  {  // direct write (fra_dw.h): 16-bit plans without mid-side, one frame group -- opt-in (FRA_DW=1): measured
-     // slower than the slot path on C4 (look-back waits)
-    const char* ev = getenv("FRA_DW");
-    const bool want = ev && atoi(ev) != 0 && analyze_dw_capable() && !p->b32 && !ms && p->groups.size() == 1 &&
-                      nfr > 0 && (int64_t)nfr * p->cmax < INT32_MAX;
-    if (want) {
-      p->lb_bytes = 2 * sizeof(unsigned long long) * (size_t)nfr * p->cmax;
-      HIPCHK(hipMalloc(&p->d_lb, p->lb_bytes));
-      HIPCHK(hipMemsetAsync(p->d_lb, 0, p->lb_bytes, p->ctx->stream));  // (ordered before the launches)
-      HIPCHK(hipMalloc(&p->d_hdr, sizeof(uint32_t) * 4 * (size_t)nfr));
-      HIPCHK(hipMalloc(&p->d_hbytes, (size_t)nfr + 1));
-      HIPCHK(hipMalloc(&p->d_abort, sizeof(int)));
-      HIPCHK(hipMemsetAsync(p->d_abort, 0, sizeof(int), p->ctx->stream));
-      HIPCHK(hipHostMalloc((void**)&p->h_abort, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-      *p->h_abort = 0;
-      int* dab = nullptr;
-      HIPCHK(hipHostGetDevicePointer((void**)&dab, p->h_abort, 0));
-      HIPCHK(hipMalloc(&p->d_dwctl, sizeof(DwCtl)));
-      HIPCHK(hipMalloc(&p->d_dwdiag, 8 * sizeof(unsigned long long)));
-      HIPCHK(hipMemsetAsync(p->d_dwdiag, 0, 8 * sizeof(unsigned long long), p->ctx->stream));
-      const char* tm = getenv("FRA_DW_TIMEOUT");  // s_memrealtime ticks (100 MHz)
-      if (getenv("FRA_DW_TRACE")) {
-        HIPCHK(hipMalloc(&p->d_dwtrace, 4 * sizeof(unsigned long long) * (size_t)nfr * p->cmax));
-        HIPCHK(hipMemsetAsync(p->d_dwtrace, 0, 4 * sizeof(unsigned long long) * (size_t)nfr * p->cmax, p->ctx->stream));
-      }
-      p->hdw = DwCtl{p->d_lb, p->d_gbase, nullptr, p->d_hdr, p->d_hbytes, p->d_abort, dab, p->d_dwdiag,
-                     tm ? (unsigned long long)atoll(tm) : 2000000ull, p->d_dwtrace};
-      HIPCHK(hipMemcpy(p->d_dwctl, &p->hdw, sizeof(DwCtl), hipMemcpyHostToDevice));
-      HIPCHK(launch_frame_headers(p->d_streams, p->d_frames, nfr, p->d_hdr, p->d_hbytes, p->ctx->stream));
-      HIPCHK(hipStreamSynchronize(p->ctx->stream));
-      p->dw = true;
-      if (const char* e0 = getenv("FRA_DW_EPOCH0")) p->epoch = (uint32_t)atoi(e0) & 0xFFFFu;  // (tests: wrap)
-    }
-  }
   return FRA_OK;
 }
 
@@ -763,35 +690,21 @@ static int drain_pipeline(fra_plan* p) {
       HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_pack[b], 0));
       p->pack_pending[b] = false;
     }
-    p->ana_pending[b] = false;  // (analyses run on the plan's stream itself)
+    p->ana_pending[b] = false;  // (covered by the resync below)
   }
-  p->raster_dirty = false;     // later norm stages run on the plan's stream, after the copy
+  // serial executes and host raster copies now go onto the plan's stream; when pipelining resumes, the
+  // first background norm stage waits for ALL of it (an event recorded on the plan's stream at that
+  // point): a pipelined analysis still reading a norm set or a raster copy queued before this drain
+  // cannot be overtaken
+  p->resync = true;
+  p->raster_dirty = false;
   use_buffers(p, 0);
   return FRA_OK;
-}
-// a direct-write look-back wait timed out (fra_dw.h): the plan continues on the slot path
-static bool dw_aborted(fra_plan* p) {
-  if (!p->dw || !p->h_abort || !*(volatile int*)p->h_abort) return false;
-  unsigned long long d[8] = {};
-  (void)hipMemcpy(d, p->d_dwdiag, sizeof(d), hipMemcpyDeviceToHost);
-  fprintf(stderr,
-          "flac_raster_amd: direct-write look-back timed out; the plan is redone on the slot path "
-          "(first: subframe %llu of the launch, ballots inc %llx ok %llx, waited %llu ticks, epoch %llu, P %llu, "
-          "bits %llu; %llu aborted)\n",
-          d[0] - 1, d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
-  p->dw = false;
-  *(volatile int*)p->h_abort = 0;
-  (void)hipMemsetAsync(p->d_abort, 0, sizeof(int), p->ctx->stream);
-  return true;
 }
 static int plan_sync_all(fra_plan* p) {
   if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
   if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));
-  if (dw_aborted(p)) {  // redo the last execute (same raster, same inputs) without direct write
-    if (int rc = fra_plan_execute(p)) return rc;
-    return plan_sync_all(p);
-  }
   return FRA_OK;
 }
 
@@ -899,28 +812,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   JobArgs ga = a;
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
-  if (p->dw) {  // direct write: k_analyze also places the frames, their CRC-16 and offsets (fra_dw.h)
-    if (++p->epoch > 0xFFFFu) {  // look-back words carry a 16-bit launch epoch
-      HIPCHK(hipMemsetAsync(p->d_lb, 0, p->lb_bytes, st));
-      p->epoch = 1;
-    }
-    ga.tmp = reinterpret_cast<uint32_t*>(p->d_dwctl);
-    ga.tmp_stride = (int64_t)p->epoch | ((int64_t)gi << 16) | ((int64_t)(gi == ng - 1 ? 1 : 0) << 47);
-    if (nf > 0) HIPCHK(launch_analyze(p->src, false, false, true, ga, st));
-    else
-      HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, 0, gi == ng - 1, a.nframes_total,
-                                  st, host_mirror));
-    if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
-    if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));
-    if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
-    if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
-    if (pack_st) {  // (keeps the pack-stream events of pipelined plans ordered after this launch)
-      HIPCHK(hipEventRecord(ev_scan, st));
-      HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
-    }
-    return FRA_OK;
-  }
-  HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, false, ga, st));
+  HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st));
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
   HIPCHK(launch_frame_bytes(ga, st));
@@ -963,6 +855,11 @@ int fra_plan_execute(fra_plan* p) {
     // norm stage of this execute on the norm stream: after execute k-2's analysis read set b, and after a
     // host raster copy enqueued on the plan's stream since the last execute
     if (p->ana_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_ana[b], 0));
+    if (p->resync) {  // first pipelined execute after serial ones: after everything on the plan's stream
+      HIPCHK(hipEventRecord(p->ev_raster, s));
+      p->raster_dirty = true;
+      p->resync = false;
+    }
     if (p->raster_dirty) {
       HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_raster, 0));
       p->raster_dirty = false;
@@ -1098,16 +995,13 @@ int fra_plan_set_first_frame(fra_plan* p, int32_t first_frame) {
   if (!p->streams.empty())  // ordered before the next execute on the plan's stream
     HIPCHK(hipMemcpyAsync(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(),
                           hipMemcpyHostToDevice, p->ctx->stream));
-  if (p->dw)  // frame numbers are part of the static headers
-    HIPCHK(launch_frame_headers(p->d_streams, p->d_frames, (int)p->frames.size(), p->d_hdr, p->d_hbytes,
-                                p->ctx->stream));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));  // the host array may change again before it is read
   return FRA_OK;
 }
 
 int fra_plan_flags(fra_plan* p, int32_t* flags) {
   if (!p || !flags) return set_err(FRA_E_INVALID, "null argument");
-  *flags = (p->dw ? FRA_PLAN_DIRECT_WRITE : 0) | (p->pipe ? FRA_PLAN_PIPELINED : 0);
+  *flags = p->pipe ? FRA_PLAN_PIPELINED : 0;
   return FRA_OK;
 }
 
@@ -1168,10 +1062,6 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
     HIPCHK(hipHostMalloc((void**)&p->h_gbase, sizeof(unsigned long long) * (nb + 1),
                          hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&p->d_gbase_mirror, p->h_gbase, 0));
-    if (p->d_dwctl) {
-      p->hdw.host_mirror = p->d_gbase_mirror;
-      HIPCHK(hipMemcpy(p->d_dwctl, &p->hdw, sizeof(DwCtl), hipMemcpyHostToDevice));
-    }
   }
   // experiment knobs (defaults = measured best): FRA_H2D_AHEAD bands of H2D ahead of the oldest band whose
   // D2H is not yet issued (0 = unlimited; 1 measured best on C4: 21.3 vs 22.2 ms)
@@ -1229,7 +1119,6 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
   }
   HIPCHK(hipStreamSynchronize(p->d2h));
   HIPCHK(hipStreamSynchronize(s));
-  if (dw_aborted(p)) return fra_plan_encode_host(p, host_raster, host_out, capacity, total_bytes);
   p->executed = true;
   if (total_bytes) *total_bytes = beg;
   if (over)

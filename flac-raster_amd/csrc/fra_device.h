@@ -15,6 +15,10 @@
 
 namespace fra {
 
+#ifndef FRA_LOAD_STAMP
+#define FRA_LOAD_STAMP(k, dep)  // diagnostic hook (fra_analyze.hip, FRA_STAMPS_FINE builds only)
+#endif
+
 // ---------------------------------------------------------------- ordered keys for nanmin/nanmax
 __device__ __forceinline__ unsigned long long okey(double v) {
   unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -241,12 +245,14 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
   auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
   T raw[K];
   load_raw_t<SRC, VEC, SmpT>(base, st, fr, c, raw);
+  FRA_LOAD_STAMP(12, (int)raw[0] + (int)raw[K - 1])
   if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
     if (lut) {  // <= 16-bit integers: the normalised sample of value mn + d is lut[d] (k_norm_lut)
       const int mnint = (int)np.mn;
       int32_t v[K];
 #pragma unroll
       for (int k = 0; k < K; k++) v[k] = lut[(int)raw[k] - mnint];
+      FRA_LOAD_STAMP(13, v[0] + v[K - 1])
 #pragma unroll
       for (int k = 0; k < K; k++) {
         const int i = sidx_of(k);

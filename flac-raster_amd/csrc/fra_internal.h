@@ -180,31 +180,6 @@ constexpr int kHdrWords = 6;
 constexpr int kMetaWords = 16;
 static_assert(kHdrWords + kMaxChannels + 2 <= kMetaWords, "frame metadata layout");
 
-// x^e mod P for e in [0, kXOrd) (u16 each), appended to the CRC-16 tables: x has order 32767 modulo
-// x^16+x^15+x^2+1, so every power (and x^-e = x^(kXOrd - e)) is one table entry
-constexpr int kXpowOff = kCrcT16Off + 16 * 256;
-constexpr int kXOrd = 32767;
-
-// Direct write: the 16-bit k_analyze places every encoded subframe at its final bit offset
-// in the output (decoupled look-back over the subframes in frame-major launch order), CRC-16 combined from
-// per-subframe residues, so no slot round trip and no k_frame_bytes/scan/k_assemble.  Static per plan,
-// in device memory; a direct-write launch passes it in JobArgs::tmp and packs
-// epoch | grp << 16 | last_grp << 47 into JobArgs::tmp_stride (kernel arguments unchanged).
-struct DwCtl {
-  unsigned long long* lb;           // [2 * nframes_total * cmax]: per subframe the look-back word
-                                    //   {epoch:16 | inclusive:1 | value:47} and the residue word
-                                    //   {epoch:16 | bits:24 | last 8 bits:8 | CRC-16 residue:16}
-  unsigned long long* gbase;        // byte offset of each launch's first frame (launch grp writes grp + 1)
-  unsigned long long* host_mirror;  // page-locked mirror of gbase (host pipeline) or null
-  const uint32_t* hdr;              // [nframes_total][4] frame header incl. CRC-8, big-endian words
-  const uint8_t* hbytes;            // [nframes_total + 1] header bytes per frame (0 past the end)
-  int* abort_dev;                   // set when a look-back wait timed out (the launch is then redone)
-  int* abort_host;                  // page-locked mirror of abort_dev
-  unsigned long long* diag;         // [8] first aborting subframe: li + 1, ballots, ticks waited, ...
-  unsigned long long timeout;       // look-back wait limit in s_memrealtime ticks
-  unsigned long long* trace;        // optional [launch subframes][4] s_memrealtime stamps (FRA_DW_TRACE)
-};
-
 struct JobArgs {
   const void* raster;
   const StreamDev* streams;

@@ -219,40 +219,6 @@ __global__ void k_frame_bytes(JobArgs a) {
   a.frame_bytes[g] = ((uint64_t)(bits + 7) >> 3) + 2;
 }
 
-// direct write (fra_dw.h): every frame's header as k_frame_bytes builds it for independent channels --
-// static per plan (frame number, block size, sample rate, bps), computed once -- as big-endian words,
-// and its length in bytes (entry nframes = 0)
-__global__ void k_frame_headers(const StreamDev* streams, const FrameDev* frames, int nframes, uint32_t* hdr,
-                                uint8_t* hbytes) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g > nframes) return;
-  if (g == nframes) {
-    hbytes[g] = 0;
-    return;
-  }
-  const FrameDev fr = frames[g];
-  const StreamDev st = streams[fr.stream];
-  uint8_t h[4 * 4];
-  int hl = frame_header(h, st, fr, st.channels - 1);
-  uint32_t c8 = 0;  // CRC-8 (RFC 9639 9.1.8)
-  for (int i = 0; i < hl; i++) {
-    c8 ^= h[i];
-    for (int b = 0; b < 8; b++) c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) & 0xFF : (c8 << 1);
-  }
-  h[hl++] = (uint8_t)c8;
-  uint32_t w[4] = {0u, 0u, 0u, 0u};
-  for (int b = 0; b < hl; b++) w[b >> 2] |= (uint32_t)h[b] << (24 - 8 * (b & 3));
-#pragma unroll
-  for (int j = 0; j < 4; j++) hdr[4 * (size_t)g + j] = w[j];
-  hbytes[g] = (uint8_t)hl;
-}
-
-hipError_t launch_frame_headers(const StreamDev* streams, const FrameDev* frames, int nframes, uint32_t* hdr,
-                                uint8_t* hbytes, hipStream_t s) {
-  k_frame_headers<<<(nframes + 1 + 255) / 256, 256, 0, s>>>(streams, frames, nframes, hdr, hbytes);
-  return hipGetLastError();
-}
-
 // ============================================================================ launchers
 #define FRA_SRC_CASES(M) M(ST_U8) M(ST_I8) M(ST_U16) M(ST_I16) M(ST_U32) M(ST_I32) M(ST_F32) M(ST_F64)
 

@@ -179,16 +179,26 @@ FRA_API int fra_tiff_decode(const uint8_t* file, uint64_t file_len, const fra_ti
     if (c.offset > file_len || c.bytes > file_len - c.offset || c.rows < 0 || c.cols < 0 ||
         (spp == 1 && (c.plane < 0 || c.plane >= L->bands)))
       return fra_internal_set_error(FRA_E_INVALID, "TIFF chunk %d out of the file / bad geometry", i);
+    // decoded chunk size rows * cols * spp * es from untrusted tags: no 64-bit wrap, and no more than the
+    // stored bytes can hold -- uncompressed: their count (checked again per chunk); LZW/deflate: at most
+    // 4096 decoded bytes per stored byte (a 12-bit LZW code expands to <= 4096 bytes; deflate <= 1032),
+    // so a malformed file is an error, not a huge allocation
+    uint64_t need = 0;
+    const uint64_t cap = comp == 1 ? c.bytes : c.bytes * 4096ull + 65536ull;
+    if (__builtin_mul_overflow((uint64_t)c.cols, (uint64_t)spp * (uint64_t)es, &need) ||
+        __builtin_mul_overflow(need, (uint64_t)c.rows, &need) || need > cap)
+      return fra_internal_set_error(FRA_E_INVALID, "TIFF chunk %d: %d x %d x %d samples do not fit its %llu stored bytes",
+                                    i, c.rows, c.cols, spp, (unsigned long long)c.bytes);
   }
   int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
   nt = std::max(1, std::min({nt, 64, std::max(1, (int)nchunks)}));
   std::atomic<int> next{0};
   std::atomic<int> failed{-1};
   std::atomic<int> why{0};
-  auto work = [&]() {
-    std::vector<uint8_t> buf, tmp;
+  auto work_body = [&](std::vector<uint8_t>& buf, std::vector<uint8_t>& tmp, int& cur) {
     for (;;) {
       const int i = next.fetch_add(1);
+      cur = i;
       if (i >= nchunks || failed.load() >= 0) return;
       const fra_tiff_chunk& c = chunks[i];
       const size_t row_bytes = (size_t)c.cols * spp * es;
@@ -253,6 +263,18 @@ FRA_API int fra_tiff_decode(const uint8_t* file, uint64_t file_len, const fra_ti
       }
     }
   };
+  // no exception may leave a worker thread (std::terminate) or cross the C ABI: report it as a failure
+  auto work = [&]() {
+    std::vector<uint8_t> buf, tmp;
+    int cur = -1;
+    try {
+      work_body(buf, tmp, cur);
+    } catch (...) {
+      int expect = -1;
+      failed.compare_exchange_strong(expect, std::max(0, cur));
+      why = 4;
+    }
+  };
   if (nt == 1) {
     work();
   } else {
@@ -265,7 +287,8 @@ FRA_API int fra_tiff_decode(const uint8_t* file, uint64_t file_len, const fra_ti
     const int w = why.load();
     return fra_internal_set_error(FRA_E_INVALID, "TIFF chunk %d: %s", failed.load(),
                                   w == 1 ? "truncated uncompressed chunk"
-                                         : (w == 3 ? "old-style (LSB-first) LZW is not supported" : "corrupt compressed data"));
+                                         : (w == 3 ? "old-style (LSB-first) LZW is not supported"
+                                                  : (w == 4 ? "out of memory" : "corrupt compressed data")));
   }
   return FRA_OK;
 }

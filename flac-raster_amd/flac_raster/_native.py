@@ -18,7 +18,7 @@ import numpy as np
 # FRA_LIB_PATH: load another build of the library (same-box A/B experiments, tools/gpu_ab.sh)
 _LIB_PATH = Path(os.environ.get("FRA_LIB_PATH") or Path(__file__).resolve().parent / "_lib" / "libflac_raster_amd.so")
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()  # re-entrant: __del__ (cyclic GC) may run while this thread holds it
 
 DTYPE_CODES = {
     np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16): 3,
@@ -171,7 +171,7 @@ def stream_header(channels: int, bps: int, sample_rate: int, blocksize: int = 40
 
 _PIN_POOL_BYTES = int(os.environ.get("FRA_PINNED_POOL_MB", "8192")) << 20
 _pin_pool: List[Tuple[int, int]] = []  # (capacity, ptr) of released page-locked blocks kept for reuse
-_pin_lock = threading.Lock()
+_pin_lock = threading.RLock()  # re-entrant, as _lock
 
 
 class _PinnedBlock:

@@ -147,7 +147,8 @@ class StreamEncoder:
         if nblk:
             self._encode_emit(pend[: nblk * self._bs])
             pend = pend[nblk * self._bs:]
-        self._pending = pend.copy() if pend.base is not None else pend
+        # always an own copy (<= blocksize rows): the caller may refill its buffer before the next call
+        self._pending = pend.copy()
 
     def finish(self) -> bool:
         if not self._initialised:

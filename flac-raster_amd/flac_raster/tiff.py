@@ -140,7 +140,11 @@ class GeoTIFF:
         if self.tiled:
             self.cw, self.ch = int(t[322][0]), int(t[323][0])
         else:
-            self.cw, self.ch = W, int(t.get(278, [H])[0])
+            self.cw, self.ch = W, min(int(t.get(278, [H])[0]), H)  # RowsPerStrip 2^32-1 = one strip
+        # chunk geometry comes from untrusted tags: positive and at most 2^20 on a side (the native decoder
+        # re-checks every chunk's decoded size with overflow-safe arithmetic against its stored bytes)
+        if not (0 < self.cw <= (1 << 20) and 0 < self.ch <= (1 << 20)):
+            raise ValueError(f"TIFF chunk geometry {self.cw} x {self.ch} is not supported")
         self.nx = (W + self.cw - 1) // self.cw
         self.ny = (H + self.ch - 1) // self.ch
 

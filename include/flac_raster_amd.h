@@ -140,9 +140,9 @@ FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_
 FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
 FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
-/* how the plan encodes (FRA_PLAN_*): direct write = k_analyze places each subframe at its final offset,
- * CRC-16 and frame offsets included (16-bit plans without mid-side); otherwise subframe slots +
- * k_frame_bytes + k_assemble.  A plan whose direct-write look-back ever timed out reports the slot path. */
+/* how the plan encodes (FRA_PLAN_*): PIPELINED = executes overlap (double-buffered subframe slots, the
+ * next execute's normalisation stage and this one's assembly run beside k_analyze).  FRA_PLAN_DIRECT_WRITE
+ * is never set (the direct-write path was measured slower than slots + k_assemble and removed in r03). */
 #define FRA_PLAN_DIRECT_WRITE 1
 #define FRA_PLAN_PIPELINED 2
 FRA_API int fra_plan_flags(fra_plan *plan, int32_t *flags);

@@ -128,6 +128,22 @@ def test_stream_encoder_incremental_emission(golden_dir):
     assert b"".join(c[0] for c in calls) == O.encode(audio, 44100, level=5)
 
 
+def test_stream_encoder_reused_input_buffer(golden_dir):
+    """One caller buffer refilled between process() calls of <= blocksize samples (sf.read(out=buf)
+    shape): the look-ahead samples the encoder keeps must be its own copy."""
+    audio = _rgb_audio(golden_dir)
+    out = bytearray()
+    enc = StreamEncoder(44100, lambda b, n, s, f: out.extend(b), compression_level=5, blocksize=4096)
+    buf = np.empty((3000, 3), np.int16)
+    for a in range(0, len(audio), len(buf)):
+        part = audio[a:a + len(buf)]
+        buf[:len(part)] = part
+        enc.process(buf[:len(part)])
+        buf.fill(0x5A5A)  # the caller reuses its buffer
+    enc.finish()
+    assert bytes(out) == O.encode(audio, 44100, level=5)
+
+
 def test_stream_encoder_multi_process_and_defaults(golden_dir):
     audio = _rgb_audio(golden_dir)
     out = bytearray()

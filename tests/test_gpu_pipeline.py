@@ -138,6 +138,16 @@ def test_cross_execute_pipelining_buffers():
             total = plan.encode_host(r, out)  # drains the pipelined execute, then the host bands
             assert bytes(out[:total]) == outs[0][1]
             assert plan.frame_offsets(sum(i.nframes for i in outs[0][0]))[-1] == total
+            # pipelined -> serial (timing) -> pipelined with no host sync anywhere (the first
+            # pipelined norm stage after serial work must wait for the plan's stream)
+            plan.execute()
+            plan.enable_timing(True)
+            plan.execute()
+            plan.enable_timing(False)
+            plan.execute()
+            plan.execute()
+            plan.sync()
+            assert plan.download()[1] == outs[0][1]
         finally:
             plan.close()
     finally:
