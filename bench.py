@@ -335,6 +335,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of 1-core CPU oracle work (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="time rank R's LPT share of the scene for an N-GPU strong-scaling run, on this one GPU "
+                         "(projection of the multi-GPU step; DESIGN.md section 7)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
     ap.add_argument("--no-trace", action="store_true", help="skip the in-run rocprofv3 kernel-trace pass")
@@ -389,7 +392,15 @@ def main():
     weak = args.scaling == "weak"
     ctx.synth(cfg["kind"], SEED + (rank if weak else 0), B, H, W, dev_raster)
     wins = tiles(H, W, cfg["tile"])
-    owner = [rank] * len(wins) if weak else lpt_shard(wins, world)
+    shard_of = None
+    if args.shard:
+        sr, sn = (int(x) for x in args.shard.split("/"))
+        if world != 1 or not 0 <= sr < sn:
+            raise SystemExit("--shard R/N needs a single process and 0 <= R < N")
+        shard_of = (sr, sn)
+    owner = ([rank] * len(wins) if weak else lpt_shard(wins, world)) if shard_of is None else lpt_shard(wins, shard_of[1])
+    if shard_of is not None:
+        rank = shard_of[0]
     mine = [i for i in range(len(wins)) if owner[i] == rank]
     my_wins = [wins[i] for i in mine]
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
@@ -440,6 +451,20 @@ def main():
     step_ms_local = sum(per_launch_ms)
     path_gbps = alg_bytes / (step_ms_local * 1e-3) / 1e9
 
+    if shard_of is not None:  # projection line: this rank's share only, not a job throughput
+        sh = {"shard": f"{shard_of[0]}/{shard_of[1]}", "config": cfg["workload"], "tiles": len(my_wins),
+              "pixels": my_px, "ms_per_step": round(T / args.steps * 1e3, 4),
+              "kernel_ms_per_launch": {"minmax": round(per_launch_ms[0], 4), "analyze": round(per_launch_ms[1], 4),
+                                       "frame_bytes+scan": round(per_launch_ms[2], 4),
+                                       "pack": round(per_launch_ms[3], 4)},
+              "fixed_ms_per_step": round(T / args.steps * 1e3 - per_launch_ms[1], 4),
+              "projected_job_mpix_s": round(H * W / (T / args.steps) / 1e6, 2),
+              "note": "projected, unmeasured on hardware: one GPU runs this rank's LPT tile share of the scene; "
+                      "the N-GPU step is the slowest rank's step (LPT imbalance <= 1.022 on C4)"}
+        print(json.dumps(sh), flush=True)
+        plan.close()
+        ctx.free(dev_raster)
+        return
     result = None
     if rank == 0:
         scene_px = H * W

@@ -244,6 +244,55 @@ __device__ __forceinline__ void q_pairs(const int32_t* q, fra_short2 (&Q)[NP]) {
 #pragma unroll
   for (int p = 0; p < NP; p++) Q[p] = pack_pair(q[2 * p], q[2 * p + 1]);
 }
+// 16-bit path straight from the LDS words: D[j] = samples (x[2j], x[2j+1]) as (lo, hi) int16, x[k] = sample
+// i0 - 12 + k.  The dot2 operand pairs are taken in memory order (x[k], x[k+1]) -- a word itself for even k,
+// one v_alignbit for odd k -- against coefficient pairs in reversed order (q[2p+1], q[2p]), so no sample
+// is unpacked to 32 bits and re-packed
+__device__ __forceinline__ void read_d14(const int16_t* smp, int t, uint32_t (&D)[14]) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(smp);  // kSmpStride even: chunks start dword-aligned
+#pragma unroll
+  for (int j = 0; j < 6; j++) D[j] = d[(t * kSmpStride + 4) / 2 + j];
+#pragma unroll
+  for (int j = 0; j < 8; j++) D[6 + j] = d[(t + 1) * kSmpStride / 2 + j];
+}
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&D)[14], int k) {
+  return (k & 1) ? __builtin_amdgcn_alignbit(D[(k + 1) >> 1], D[(k - 1) >> 1], 16) : D[k >> 1];
+}
+__device__ __forceinline__ int32_t sample_at(const uint32_t (&D)[14], int k) {
+  return (k & 1) ? hi16(D[k >> 1]) : lo16(D[k >> 1]);
+}
+template <int NP>
+__device__ __forceinline__ void q_pairs_rev(const int32_t* q, fra_short2 (&Q)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; p++) Q[p] = pack_pair(q[2 * p + 1], q[2 * p]);
+}
+// prediction of x[b]: sum_p dot2((x[b-2-2p], x[b-1-2p]), (q[2p+1], q[2p]))
+template <int NP>
+__device__ __forceinline__ int32_t pred_raw(const uint32_t (&D)[14], int b, const fra_short2 (&Q)[NP]) {
+  int32_t acc = 0;
+#pragma unroll
+  for (int p = 0; p < NP; p++)
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(fra_short2, pair_at(D, b - 2 - 2 * p)), Q[p], acc, false);
+  return acc;
+}
+// sum of |residual| of order O over the thread's 16 samples (warm-up positions jj < O of thread 0 masked),
+// the residuals kept in r for the winner's encode
+template <int O>
+__device__ __forceinline__ uint32_t lpc_abs16_raw(const uint32_t (&D)[14], const int32_t* q, int sh, bool head,
+                                                  int32_t (&r)[kChunk]) {
+  constexpr int NP = (O + 1) / 2;
+  fra_short2 Q[NP];
+  q_pairs_rev<NP>(q, Q);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int jj = 0; jj < kChunk; jj++) {
+    r[jj] = sample_at(D, 12 + jj) - (pred_raw<NP>(D, 12 + jj, Q) >> sh);
+    const uint32_t rb = (uint32_t)r[jj] ^ kBias;
+    acc = sad_acc(rb, (jj < O && head) ? rb : kBias, acc);
+  }
+  return acc;
+}
+
 // 16-bit path: sum of |LPC residual| over the thread's 16 samples (|r| < 2^27: fits 32 bits), warm-up
 // positions jj < O masked for thread 0 only (compile-time bound); the caller doubles it (3.8)
 template <int O>
@@ -396,8 +445,17 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
                                  int t) {
   for (uint32_t j = t; j < nw; j += kThreads) slot[j] = verbatim_word(smp, n, hdr, w, sbps, j);
 }
+#ifndef FRA_KEEP
+#define FRA_KEEP 1      // keep the last LPC model's residuals in registers for the winner's encode
+#endif
+#ifndef FRA_FASTLOAD
+#define FRA_FASTLOAD 1  // full-frame LUT load path (load_lut_full)
+#endif
+#ifndef FRA_WAVES16
+#define FRA_WAVES16 5   // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
+#endif
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
@@ -439,7 +497,12 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_an
     const NormParams np = norm_params(st, a.norm[fr.stream]);
     const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
     FRA_LOAD_STAMP(11, (int)np.mn + st.width + fr.n)
-    load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
+    bool done = false;
+    if constexpr (!B32) {
+      if (FRA_FASTLOAD && lut && a.vec8 && a.off32 && n == kMaxBlock)
+        done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
+    }
+    if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -541,6 +604,19 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_an
   }
   FRA_STOP(9)
   FRA_STAMP(2)
+#if defined(FRA_EXP_PAD) && FRA_EXP_PAD > 0
+  {  // diagnostic build: FRA_EXP_PAD extra independent VALU instructions per wave (4 chains of v_add_u32)
+    uint32_t p0 = t, p1 = t + 1, p2 = t + 2, p3 = t + 3;
+#pragma unroll
+    for (int k = 0; k < FRA_EXP_PAD / 4; k++) {
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p0) : "v"(p1));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p1) : "v"(p2));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p2) : "v"(p3));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p3) : "v"(p0));
+    }
+    if ((p0 ^ p1 ^ p2 ^ p3) == 0x7FFFFFF3u) S.ired[0][3] = 1;  // keep the chains alive
+  }
+#endif
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = fixfast && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
@@ -576,11 +652,14 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_an
         {
           int32_t y[kChunk + 8];
           read_y24(S.smp, t, y);
+          // no bounds select: load_window left the coefficients of samples at or past n at 0.0f, and a
+          // finite sample times +-0.0f adds +-0.0 to a chunk partial, which leaves the float sum bit-identical
+          // (x + -0.0 == x, +0.0 + -0.0 == +0.0) -- the oracle's skipped terms
 #pragma unroll
           for (int j = 0; j < kChunk + MAXLAG; j++) {
             const int i = i0 + j;
             const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
-            wf[j] = (i < n) ? (float)v * wcoef[j] : 0.0f;
+            wf[j] = (float)v * wcoef[j];
           }
         }
 
@@ -693,9 +772,12 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : 7)) k_an
 
   FRA_STOP(2)
   // ---- 4. residual partition sums at the finest level P for every valid model (3.8)
-  {  // (the fast 16-bit path's FIXED sums consumed x)
-read_x28(S.smp, t, x);
-  }
+  uint32_t D[B32 ? 1 : 14];  // 16-bit fast frames: the LDS words of the sample window (read_d14)
+  int32_t rkeep[B32 ? 1 : kChunk];  // 16-bit fast frames: residuals of the last LPC model summed (model keep_m)
+  int keep_m = -1;
+  if constexpr (B32) read_x28(S.smp, t, x);  // (the fast 16-bit path's FIXED sums consumed x)
+  else if (fastframe) read_d14(S.smp, t, D);
+  else read_x28(S.smp, t, x);
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
   FRA_STAMP(4)
   double xd[B32 ? 12 + kChunk : 1];  // 32-bps fast path: x as exact doubles
@@ -734,7 +816,7 @@ read_x28(S.smp, t, x);
   case O_:           \
     if constexpr (O_ <= MAXO) { \
       if constexpr (B32) acc = lpc_abs2_f64<O_>(xd, qd, sh, skip, ovf); \
-      else acc = 2ull * lpc_abs16<O_>(x, q, sh, head); \
+      else acc = 2ull * lpc_abs16_raw<O_>(D, q, sh, head, rkeep); \
     } \
     break;
         FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6)
@@ -744,6 +826,8 @@ read_x28(S.smp, t, x);
       if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
       if constexpr (B32) {
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
+      } else {
+        keep_m = FRA_KEEP ? m : -1;
       }
     }
   } else {
@@ -827,8 +911,28 @@ read_x28(S.smp, t, x);
       const int k0 = S.kbest[m][pidx];
       // zig-zag residuals of the winner (exact code values), warm-up samples 0
       uint32_t uu[kChunk];
-      read_x28(S.smp, t, x);
-      if (type == 2 && (!B32 || fixfast)) {  // FIXED: finite differences in 32 bits (range checked)
+      bool have = false;
+      if constexpr (!B32) {
+        if (m == keep_m) {  // the winner is the LPC model whose residuals are still in registers
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(rkeep[jj]);
+          have = true;
+        } else if (type == 3) {
+          int32_t q[MAXO];
+#pragma unroll
+          for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
+          fra_short2 Q[(MAXO + 1) / 2];
+          q_pairs_rev<(MAXO + 1) / 2>(q, Q);
+          read_d14(S.smp, t, D);
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++)
+            uu[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<(MAXO + 1) / 2>(D, 12 + jj, Q) >> sh));
+          have = true;
+        }
+      }
+      if (have) {
+      } else if (type == 2 && (!B32 || fixfast)) {  // FIXED: finite differences in 32 bits (range checked)
+        read_x28(S.smp, t, x);
 #pragma unroll
         for (int k = 1; k <= 4; k++) {
           if (k <= o) {
@@ -839,6 +943,7 @@ read_x28(S.smp, t, x);
 #pragma unroll
         for (int jj = 0; jj < kChunk; jj++) uu[jj] = zz32(x[12 + jj]);
       } else {
+        read_x28(S.smp, t, x);
         int32_t q[MAXO];
 #pragma unroll
         for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
@@ -997,13 +1102,14 @@ read_x28(S.smp, t, x);
         for (int ww = 0; ww < wv; ww++) p += S.scan[ww];
         if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
         // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
+        // (u << (31 - k)) keeps u's low k bits under bit 31 and shifts the higher ones out; bit 31 (u's bit
+        // k) is then forced to the stop bit: one v_lshl_or_b32, no mask
         const uint32_t sal = 31u - (uint32_t)kcur;
-        const uint32_t mal = ((1u << kcur) - 1u) << sal;
 #pragma unroll
         for (int jj = 0; jj < kChunk; jj++) {
           if (live && !(jj < 12 && head && jj < o)) {
             const uint32_t P = p + (uu[jj] >> kcur);
-            lds_put_al(buf, P, ((uu[jj] << sal) & mal) | 0x80000000u);
+            lds_put_al(buf, P, (uu[jj] << sal) | 0x80000000u);
             p = P + 1u + (uint32_t)kcur;
           }
         }
@@ -1253,12 +1359,11 @@ read_x28(S.smp, t, x);
       if (pstart) { lds_put(buf, p, (uint32_t)kcur, pb); p += pb; }
       // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
       const uint32_t sal = 31u - (uint32_t)kcur;
-      const uint32_t mal = ((1u << kcur) - 1u) << sal;
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
         if (live && !(jj < 12 && head && jj < o)) {
           const uint32_t P = p + (uu[jj] >> kcur);
-          lds_put_al(buf, P, ((uu[jj] << sal) & mal) | 0x80000000u);
+          lds_put_al(buf, P, (uu[jj] << sal) | 0x80000000u);  // (see above: no mask needed)
           p = P + 1u + (uint32_t)kcur;
         }
       }
@@ -1320,7 +1425,13 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
+#ifdef FRA_EXP_LDS
+  // diagnostic build: FRA_EXP_LDS=bytes of dynamic LDS per workgroup (lowers the workgroups per CU)
+  static const unsigned dyn = getenv("FRA_EXP_LDS") ? (unsigned)atoi(getenv("FRA_EXP_LDS")) : 0u;
+#else
+  constexpr unsigned dyn = 0;
+#endif
+#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, dyn, s>>>(a, src)
   if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
     grid.y = 2;

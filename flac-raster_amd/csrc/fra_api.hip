@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <map>
 #include <new>
 #include <string>
@@ -78,6 +79,7 @@ struct fra_plan {
   int max_segs = 0;
   int mm_vec = 0, mm_rows = 1, mm_max_rows = 0;  // vectorised k_minmax shape (0 = scalar path)
   bool ld_vec8 = false;  // k_analyze 8-byte sample vectors possible (pointer alignment checked at execute)
+  bool ld_off32 = false;  // k_analyze 32-bit lane offsets (JobArgs::off32)
   int cmax = 1;
   int ncu = 256;  // compute units of the device (background grids)
   size_t raster_bytes = 0;
@@ -500,6 +502,15 @@ static int plan_build(fra_plan* p) {
       if (st.nsamples) ok = st.base_off % V == 0 && st.width % V == 0;
     }
     p->ld_vec8 = ok;
+    // 32-bit lane offsets of the fast load path: a frame's rows of one channel span < 2^31 bytes
+    bool o32 = j.row_stride >= 0;
+    for (int w = 0; o32 && w < j.nwindows; w++) {
+      const StreamDev& st = p->streams[w];
+      if (!st.nsamples) continue;
+      const int64_t rows = (j.blocksize + st.width - 1) / st.width + 1;
+      o32 = (rows * j.row_stride + st.width) * elem_size(j.dtype) < (int64_t(1) << 31);
+    }
+    p->ld_off32 = o32;
   }
   if (nf_total > INT32_MAX / 2) return set_err(FRA_E_INVALID, "too many frames (%lld)", (long long)nf_total);
   p->raster_bytes = (size_t)max_extent * elem_size(j.dtype);
@@ -623,6 +634,7 @@ static int plan_build(fra_plan* p) {
   a.blocksize = j.blocksize;
   a.level = j.level;
   a.nwin = std::max(1, p->nwin);
+  a.off32 = p->ld_off32 ? 1 : 0;
   for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
   {  // second buffer set for cross-execute pipelining
     const char* ev = getenv("FRA_PIPE");
@@ -1031,8 +1043,31 @@ static int copy_rows_h2d(fra_plan* p, const uint8_t* host, int64_t r0, int64_t r
   return FRA_OK;
 }
 
+static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
+                       uint64_t* total_bytes, const volatile int64_t* rows_ready);
 int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
                          uint64_t* total_bytes) {
+  return encode_host(p, host_raster, host_out, capacity, total_bytes, nullptr);
+}
+int fra_plan_encode_host_progress(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
+                                  uint64_t* total_bytes, const volatile int64_t* rows_ready) {
+  if (!rows_ready) return set_err(FRA_E_INVALID, "null rows_ready");
+  return encode_host(p, host_raster, host_out, capacity, total_bytes, rows_ready);
+}
+// wait (host) until the producer has published rows [0, r1) of the raster; false if it reported failure
+static bool wait_rows(const volatile int64_t* rows_ready, int64_t r1) {
+  if (!rows_ready) return true;
+  for (int spin = 0;; spin++) {
+    const int64_t r = __atomic_load_n(const_cast<const int64_t*>(rows_ready), __ATOMIC_ACQUIRE);
+    if (r < 0) return false;
+    if (r >= r1) return true;
+    if (spin < 64) continue;
+    struct timespec ts = {0, spin < 1024 ? 2000 : 50000};
+    nanosleep(&ts, nullptr);
+  }
+}
+static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
+                       uint64_t* total_bytes, const volatile int64_t* rows_ready) {
   if (!p || (!host_raster && p->raster_bytes) || (!host_out && capacity)) return set_err(FRA_E_INVALID, "null argument");
   (void)hipSetDevice(p->ctx->device);
   hipStream_t s = p->ctx->stream;
@@ -1073,6 +1108,7 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
   const uint8_t* host = (const uint8_t*)host_raster;
   auto enqueue_copy = [&](int b) -> int {
     const auto& hb = p->hbands[b];
+    if (!wait_rows(rows_ready, hb.r1)) return set_err(FRA_E_STATE, "the raster producer failed (rows_ready < 0)");
     if (hb.r1 > hb.r0) {
       const int rc = copy_rows_h2d(p, host, hb.r0, hb.r1, p->h2d);
       if (rc) return rc;
@@ -1093,15 +1129,25 @@ int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out
     beg = end;
     return FRA_OK;
   };
+  // an error after work was enqueued (a failed producer, a HIP error): drain the three streams before
+  // returning, so no copy still reads the caller's buffers
+  auto drained = [&](int code) -> int {
+    std::string keep = g_err;
+    (void)hipStreamSynchronize(p->h2d);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(p->d2h);
+    g_err = keep;
+    return code;
+  };
   int rc = enqueue_copy(0);
-  if (rc) return rc;
+  if (rc) return drained(rc);
   for (int b = 0; b < nb; b++) {
     if (b + 1 < nb) {  // the next band's rows go over PCIe meanwhile
       while (ahead > 0 && b + 1 - issued > ahead) {
         HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
-        if ((rc = enqueue_d2h(issued++))) return rc;
+        if ((rc = enqueue_d2h(issued++))) return drained(rc);
       }
-      if ((rc = enqueue_copy(b + 1))) return rc;
+      if ((rc = enqueue_copy(b + 1))) return drained(rc);
     }
     HIPCHK(hipStreamWaitEvent(s, p->hev[2 * b], 0));
     // the band's end offset reaches h_gbase by a kernel store (k_group_offsets), not by a copy-engine

@@ -110,6 +110,15 @@ template <> struct RawType<ST_I32> { using T = int32_t; };
 template <> struct RawType<ST_F32> { using T = float; };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// normalisation-table index of a <= 16-bit integer raster value: its bit pattern as an unsigned integer
+// (k_norm_lut fills the entries of the tile's values mn..mx)
+template <int SRC, typename T>
+__device__ __forceinline__ uint32_t lut_index(T v) {
+  if constexpr (SRC == ST_U8 || SRC == ST_I8) return (uint32_t)(uint8_t)v;
+  else return (uint32_t)(uint16_t)v;
+}
 
 template <typename T, int V>
 struct alignas(sizeof(T) * V) VecT {
@@ -201,7 +210,7 @@ __device__ __forceinline__ void load_mid_side_t(const void* base, const StreamDe
   const int n = fr.n, t = threadIdx.x;
   auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
   auto audio = [&](T r) -> int32_t {
-    if (kLutType && lut) return lut[(int)r - (int)np.mn];
+    if (kLutType && lut) return lut[lut_index<SRC>(r)];
     return np.mode == 0 ? (int32_t)r : norm_sample<SRC>((double)r, np);
   };
   T raw[K];
@@ -247,11 +256,10 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
   load_raw_t<SRC, VEC, SmpT>(base, st, fr, c, raw);
   FRA_LOAD_STAMP(12, (int)raw[0] + (int)raw[K - 1])
   if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
-    if (lut) {  // <= 16-bit integers: the normalised sample of value mn + d is lut[d] (k_norm_lut)
-      const int mnint = (int)np.mn;
+    if (lut) {  // <= 16-bit integers: the normalised sample of value v is lut[lut_index(v)] (k_norm_lut)
       int32_t v[K];
 #pragma unroll
-      for (int k = 0; k < K; k++) v[k] = lut[(int)raw[k] - mnint];
+      for (int k = 0; k < K; k++) v[k] = lut[lut_index<SRC>(raw[k])];
       FRA_LOAD_STAMP(13, v[0] + v[K - 1])
 #pragma unroll
       for (int k = 0; k < K; k++) {
@@ -280,6 +288,82 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
     }
   }
 }
+// Fast path of the 16-bit instance (full 4096-sample frames of a <= 16-bit integer raster, 8-byte vectors,
+// host-checked 32-bit byte offsets JobArgs::off32): per lane 32-bit offsets from a uniform frame-row base
+// (saddr loads), LUT gathers by the raw value from a uniform table base, the samples packed as int16 pairs
+// and stored 4 at a time (ds_write_b64: a thread's 4 or 8 consecutive samples lie in one 16-sample chunk),
+// OR / min / max on the packed pairs (v_pk_min_i16 / v_pk_max_i16).  No per-sample bounds (n == 4096).
+template <int SRC>
+__device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                                const int32_t* lut, int16_t* smp, uint32_t& orv, int32_t& vmin,
+                                                int32_t& vmax) {
+  using T = typename RawType<SRC>::T;
+  constexpr int V = 8 / (int)sizeof(T);                 // samples per 8-byte vector
+  constexpr int NV = kMaxBlock / kThreads / V;          // vectors per thread
+  constexpr int step = kThreads * V;
+  using VT = VecT<T, V>;
+  const int w = st.width, t = threadIdx.x;
+  const char* b0 = (const char*)((const T*)base + st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride);
+  const uint32_t rsb = (uint32_t)st.row_stride * (uint32_t)sizeof(T);
+  int col = fr.col0 + t * V;
+  uint32_t roff = 0;
+  if (col >= w) {
+    const int q = (int)((unsigned)col / (unsigned)w);
+    col -= q * w;
+    roff = (uint32_t)q * rsb;
+  }
+  VT x[NV];
+#pragma unroll
+  for (int kv = 0; kv < NV; kv++) {
+    x[kv] = *(const VT*)(b0 + (roff + (uint32_t)col * (uint32_t)sizeof(T)));
+    col += step;
+    if (col >= w) {
+      if (w >= step) { col -= w; roff += rsb; }
+      else {
+        const int q = (int)((unsigned)col / (unsigned)w);
+        col -= q * w;
+        roff += (uint32_t)q * rsb;
+      }
+    }
+  }
+  int32_t g[NV * V];
+#pragma unroll
+  for (int kv = 0; kv < NV; kv++)
+#pragma unroll
+    for (int e = 0; e < V; e++) g[kv * V + e] = lut[lut_index<SRC>(x[kv].v[e])];
+  uint32_t orp = 0;
+  i16x2 pmin = {32767, 32767}, pmax = {-32768, -32768};
+#pragma unroll
+  for (int kv = 0; kv < NV; kv++) {
+    const int i = (t + kv * kThreads) * V;
+#pragma unroll
+    for (int h = 0; h < V / 4; h++) {
+      const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)g[kv * V + 4 * h + 1], (uint32_t)g[kv * V + 4 * h], 0x05040100u);
+      const uint32_t p1 = __builtin_amdgcn_perm((uint32_t)g[kv * V + 4 * h + 3], (uint32_t)g[kv * V + 4 * h + 2], 0x05040100u);
+      *reinterpret_cast<uint2*>(smp + sidx(i + 4 * h)) = make_uint2(p0, p1);
+      orp |= p0 | p1;
+      const i16x2 a0 = __builtin_bit_cast(i16x2, p0), a1 = __builtin_bit_cast(i16x2, p1);
+      pmin = __builtin_elementwise_min(pmin, __builtin_elementwise_min(a0, a1));
+      pmax = __builtin_elementwise_max(pmax, __builtin_elementwise_max(a0, a1));
+    }
+  }
+  // OR of the int16 patterns: same trailing zeros as the OR of the sign-extended samples
+  orv |= (orp | (orp >> 16)) & 0xFFFFu;
+  vmin = min(vmin, min((int32_t)pmin.x, (int32_t)pmin.y));
+  vmax = max(vmax, max((int32_t)pmax.x, (int32_t)pmax.y));
+}
+__device__ __forceinline__ bool load_lut_full(int src, const void* base, const StreamDev& st, const FrameDev& fr, int c,
+                                              const int32_t* lut, int16_t* smp, uint32_t& orv, int32_t& vmin,
+                                              int32_t& vmax) {
+  switch (src) {  // wave-uniform dispatch
+    case ST_U8: load_lut_full_t<ST_U8>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_I8: load_lut_full_t<ST_I8>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_U16: load_lut_full_t<ST_U16>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_I16: load_lut_full_t<ST_I16>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
+    default: return false;
+  }
+}
+
 template <typename SmpT>
 __device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const StreamDev& st, const FrameDev& fr,
                                              int c, const NormParams& np, const int32_t* lut, SmpT* smp,

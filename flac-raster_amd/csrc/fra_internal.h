@@ -196,7 +196,7 @@ struct JobArgs {
   uint32_t* fmeta;         // [nframes_total][kMetaWords]: header (+CRC-8) as big-endian words, blob bit bounds
   uint32_t* tmp;           // encoded subframes: slot (frame*cmax + channel) of tmp_stride words
   const int32_t* lut;      // normalize_to_audio table per stream (<= 16-bit integer dtypes), or null
-  int64_t lut_stride;      // entries per stream: 256 (8-bit) or 65536 (16-bit); entry d = sample of mn + d
+  int64_t lut_stride;      // entries per stream: 256 (8-bit) or 65536 (16-bit), indexed by the raw value (lut_index)
   int64_t tmp_stride;
   int32_t nframes_total;
   int32_t cmax;
@@ -204,6 +204,8 @@ struct JobArgs {
   int32_t level;
   int32_t nwin;
   int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
+  int32_t off32;           // every frame's samples of one channel lie within 2^31 bytes of its first row
+                           // (k_analyze fast load path: 32-bit lane offsets from a uniform base)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
 };

@@ -231,9 +231,10 @@ __global__ void k_norm_finalize(const StreamDev* streams, NormDev* nd, int nstre
   nd[i].range = p.range;
 }
 
-// normalize_to_audio table of a <= 16-bit integer stream: entry d = the normalised sample of the raster
-// value mn + d, d = 0..mx-mn, by the same op sequence as norm_sample (k_analyze then gathers instead of
-// evaluating the float64 map per sample).  grid (64, streams), grid-stride over d.
+// normalize_to_audio table of a <= 16-bit integer stream, indexed by the raw value itself (lut_index: the
+// value's bit pattern as an unsigned 8/16-bit integer, so k_analyze gathers with one 32-bit offset from a
+// uniform base): entry of raster value v = the normalised sample of v, for v = mn..mx (the only values the
+// tile holds), by the same op sequence as norm_sample.  grid (64, streams), grid-stride over v - mn.
 template <int SRC>
 __global__ void __launch_bounds__(256) k_norm_lut(const StreamDev* streams, const NormDev* nd, int32_t* lut,
                                                   int64_t stride) {
@@ -242,8 +243,10 @@ __global__ void __launch_bounds__(256) k_norm_lut(const StreamDev* streams, cons
   const NormParams np = norm_params(st, nd[blockIdx.y]);
   const int64_t R = (int64_t)np.range;  // integer data: mx - mn, or 1 for a constant stream
   int32_t* out = lut + (int64_t)blockIdx.y * stride;
-  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d <= R && d < stride; d += (int64_t)gridDim.x * 256)
-    out[d] = norm_sample<SRC>(np.mn + (double)d, np);
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d <= R && d < stride; d += (int64_t)gridDim.x * 256) {
+    const int v = (int)np.mn + (int)d;
+    out[lut_index<SRC>((typename RawType<SRC>::T)v)] = norm_sample<SRC>(np.mn + (double)d, np);
+  }
 }
 
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s) {

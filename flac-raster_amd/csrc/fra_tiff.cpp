@@ -118,6 +118,73 @@ int64_t inflate_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
   return got;
 }
 
+// TIFF LZW encoder, the inverse of lzw_decode: Clear first, codes MSB-first, 9..12 bits.  The decoder adds
+// one entry per code after the first and widens once its next free entry reaches 2^width - 1; the encoder
+// adds its entry one code earlier, so it widens when its own next entry reaches 2^width.  Before the table
+// could overflow (next entry 4093) a Clear restarts it.  Returns bytes written, or -1 if cap is too small.
+int64_t lzw_encode(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
+  constexpr int kHash = 1 << 14;
+  std::vector<int32_t> key(kHash);
+  std::vector<uint16_t> val(kHash);
+  uint64_t acc = 0;
+  int nbits = 0;
+  size_t o = 0;
+  bool ok = true;
+  auto emit = [&](int code, int width) {
+    acc = (acc << width) | (uint64_t)code;
+    nbits += width;
+    while (nbits >= 8) {
+      if (o >= cap) { ok = false; nbits -= 8; continue; }
+      out[o++] = (uint8_t)(acc >> (nbits - 8));
+      nbits -= 8;
+    }
+  };
+  auto reset = [&]() { std::fill(key.begin(), key.end(), -1); };
+  reset();
+  int width = 9, next = 258;
+  emit(256, width);
+  if (n == 0) {
+    emit(257, width);
+  } else {
+    int w = in[0];
+    for (size_t i = 1; i < n; i++) {
+      const int c = in[i];
+      const int32_t k = (w << 8) | c;
+      uint32_t h = ((uint32_t)k * 2654435761u) >> 18;
+      int found = -1;
+      while (key[h] >= 0) {
+        if (key[h] == k) { found = val[h]; break; }
+        h = (h + 1) & (kHash - 1);
+      }
+      if (found >= 0) { w = found; continue; }
+      emit(w, width);
+      if (next < 4093) {
+        key[h] = k;
+        val[h] = (uint16_t)next++;
+        if (next >= (1 << width) && width < 12) width++;
+      } else {
+        emit(256, width);
+        reset();
+        width = 9;
+        next = 258;
+      }
+      w = c;
+    }
+    emit(w, width);
+    // the decoder adds an entry for this code too: keep its width step in step before EOI
+    if (next < 4093) {
+      next++;
+      if (next >= (1 << width) && width < 12) width++;
+    }
+    emit(257, width);
+  }
+  if (nbits > 0) {
+    if (o >= cap) ok = false;
+    else out[o++] = (uint8_t)(acc << (8 - nbits));
+  }
+  return ok ? (int64_t)o : -1;
+}
+
 inline void bswap_inplace(uint8_t* p, size_t nelem, int es) {
   if (es == 2) {
     for (size_t i = 0; i < nelem; i++) std::swap(p[2 * i], p[2 * i + 1]);
@@ -290,6 +357,59 @@ FRA_API int fra_tiff_decode(const uint8_t* file, uint64_t file_len, const fra_ti
                                          : (w == 3 ? "old-style (LSB-first) LZW is not supported"
                                                   : (w == 4 ? "out of memory" : "corrupt compressed data")));
   }
+  return FRA_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+FRA_API uint64_t fra_tiff_compress_bound(int32_t compression, uint64_t chunk_bytes) {
+  if (compression == 8 || compression == 32946) return (uint64_t)compressBound((uLong)chunk_bytes) + 64;
+  return chunk_bytes + chunk_bytes / 2 + 64;  // LZW: <= 12 bits per input byte + Clear/EOI codes
+}
+
+FRA_API int fra_tiff_compress(int32_t compression, int32_t level, const uint8_t* src, uint64_t chunk_bytes,
+                              int32_t nchunks, uint8_t* dst, uint64_t dst_stride, uint64_t* sizes, int32_t threads) {
+  if ((!src || !dst || !sizes) && nchunks > 0) return fra_internal_set_error(FRA_E_INVALID, "null argument");
+  if (compression != 5 && compression != 8 && compression != 32946)
+    return fra_internal_set_error(FRA_E_INVALID, "compression %d not supported (5 LZW, 8 deflate)", compression);
+  if (dst_stride < fra_tiff_compress_bound(compression, chunk_bytes))
+    return fra_internal_set_error(FRA_E_INVALID, "dst_stride below fra_tiff_compress_bound");
+  int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+  nt = std::max(1, std::min({nt, 64, std::max(1, (int)nchunks)}));
+  std::atomic<int> next{0};
+  std::atomic<int> failed{-1};
+  auto work = [&]() {
+    try {
+      for (;;) {
+        const int i = next.fetch_add(1);
+        if (i >= nchunks || failed.load() >= 0) return;
+        const uint8_t* in = src + (size_t)i * chunk_bytes;
+        uint8_t* out = dst + (size_t)i * dst_stride;
+        if (compression == 5) {
+          const int64_t got = lzw_encode(in, chunk_bytes, out, dst_stride);
+          if (got < 0) { failed = i; return; }
+          sizes[i] = (uint64_t)got;
+        } else {
+          uLongf got = (uLongf)dst_stride;
+          if (compress2(out, &got, in, (uLong)chunk_bytes, level < 0 ? Z_DEFAULT_COMPRESSION : level) != Z_OK) {
+            failed = i;
+            return;
+          }
+          sizes[i] = (uint64_t)got;
+        }
+      }
+    } catch (...) {
+      int expect = -1;
+      failed.compare_exchange_strong(expect, 0);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  if (failed.load() >= 0) return fra_internal_set_error(FRA_E_INVALID, "TIFF chunk %d: compression failed", failed.load());
   return FRA_OK;
 }
 

@@ -139,14 +139,46 @@ def shard(tiles: Sequence[Tuple[int, int, int, int]], world: int, rank: int) -> 
 EncodeFn = Callable[..., List[TileStream]]
 
 
+def read_rank_mosaic(src, windows: Sequence[Tuple[int, int, int, int]], pinned: bool = False):
+    """Decode ONLY ``windows`` of a GeoTIFF (path or open ``GeoTIFF``) into one rank-local band-planar
+    mosaic: window k at rows [off_k, off_k + h_k), columns [0, w_k) (stacked top to bottom; page-locked
+    when ``pinned``).  Returns ``(mosaic, local_windows)``; every local window holds exactly the pixels of
+    its source window, so its FLAC stream is byte-identical (the rasterio ``read(window=...)`` per tile of
+    ``cli.py:559``, here one decode per window straight into the rank's buffer)."""
+    from .tiff import GeoTIFF, _alloc
+
+    g = src if isinstance(src, GeoTIFF) else GeoTIFF(src)
+    try:
+        rows = sum(h for (_, _, h, _) in windows)
+        width = max((w for (_, _, _, w) in windows), default=0)
+        mosaic = _alloc((g.info.count, max(1, rows), max(1, width)), g.info.dtype, pinned)
+        local = []
+        off = 0
+        for (r0, c0, h, w) in windows:
+            g.read_window_into(mosaic[:, off:off + h, :w], r0, c0, h, w)
+            local.append((off, 0, h, w))
+            off += h
+        return mosaic, local
+    finally:
+        if g is not src:
+            g.close()
+
+
 def encode_tiles_distributed(raster, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,
                              d: Optional[Dist] = None, encode_fn: EncodeFn = encode_tiles,
                              dst: int = 0) -> Optional[List[TileStream]]:
     """Each rank encodes its LPT share on its local GPU; ``dst`` receives every stream in tile order
-    (other ranks get ``None``).  Bytes are identical for any world size."""
+    (other ranks get ``None``).  Bytes are identical for any world size.  ``raster`` is an in-memory
+    (bands, H, W) array, or a GeoTIFF path / ``GeoTIFF``: then every rank decodes only its own tiles'
+    windows (``read_rank_mosaic``), never the whole scene."""
     d = d or Dist()
     mine = shard(tiles, d.world, d.rank)
-    streams = encode_fn(raster, [tiles[i] for i in mine], level, [d.local_rank]) if mine else []
+    if isinstance(raster, (str, os.PathLike)) or type(raster).__name__ == "GeoTIFF":
+        mosaic, local = read_rank_mosaic(raster, [tiles[i] for i in mine], pinned=encode_fn is encode_tiles)
+        streams = encode_fn(mosaic, local, level, [d.local_rank]) if mine else []
+        del mosaic
+    else:
+        streams = encode_fn(raster, [tiles[i] for i in mine], level, [d.local_rank]) if mine else []
     parts = d.gather_streams(list(zip(mine, streams)), dst)
     if d.rank != dst:
         return None

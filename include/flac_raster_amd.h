@@ -136,6 +136,13 @@ FRA_API void fra_plan_destroy(fra_plan *plan);
  * host_out.  A plan's capacity bound: fra_plan_capacity. */
 FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
                                  uint64_t *total_bytes);
+/* The same pipelined pass over a raster that is still being produced (file-to-container path: a decoder
+ * thread fills host_raster top to bottom, cli.py:553-559 reads each tile's window before its encode):
+ * before the H2D copy of a row band is enqueued, the call waits until *rows_ready >= the band's last row
+ * + 1 (the producer publishes rows with a release store; -1 = the producer failed: FRA_E_STATE).  Rows
+ * are image rows of the job's raster (row_stride units). */
+FRA_API int fra_plan_encode_host_progress(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
+                                          uint64_t *total_bytes, const volatile int64_t *rows_ready);
 /* frame number of every stream's first frame for the next execute (the job's first_frame until set) */
 FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
@@ -220,6 +227,16 @@ typedef struct {
 } fra_tiff_layout;
 FRA_API int fra_tiff_decode(const uint8_t *file, uint64_t file_len, const fra_tiff_layout *layout,
                             const fra_tiff_chunk *chunks, int32_t nchunks, void *dst, int32_t threads);
+
+/* GeoTIFF chunk encoder (host, multi-threaded; the write side of the raster I/O, replacing rasterio's
+ * tile GeoTIFF writes at cli.py:577-591 / converter.py flac_to_tiff): nchunks raw chunks of chunk_bytes
+ * each, contiguous in src (already in file layout, predictor applied by the caller), are compressed with
+ * compression 5 (TIFF LZW, MSB-first, early change -- what fra_tiff_decode and libtiff read) or 8 (zlib
+ * deflate at `level`); chunk i goes to dst + i * dst_stride (dst_stride >= fra_tiff_compress_bound) and its
+ * size to sizes[i]. */
+FRA_API uint64_t fra_tiff_compress_bound(int32_t compression, uint64_t chunk_bytes);
+FRA_API int fra_tiff_compress(int32_t compression, int32_t level, const uint8_t *src, uint64_t chunk_bytes,
+                              int32_t nchunks, uint8_t *dst, uint64_t dst_stride, uint64_t *sizes, int32_t threads);
 
 /* device memory helpers for hosts without a GPU array library */
 FRA_API int fra_device_alloc(fra_ctx *ctx, uint64_t bytes, void **dev_ptr);

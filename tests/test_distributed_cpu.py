@@ -29,7 +29,7 @@ def _raster():
     return (base - base.min()).astype(np.int16)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, from_file=False):
     for p in (HERE.parent / "flac-raster_amd", HERE.parent / "oracle", HERE):
         sys.path.insert(0, str(p))
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -47,11 +47,12 @@ def _worker(rank, world, port, out_dir):
     assert d.allsum(len(mine)) == len(tiles)
     assert d.allmax(float(rank)) == float(world - 1)
     d.barrier()
-    streams = encode_tiles_distributed(r, tiles, 5, d, encode_fn=oracle_encode_tiles)
+    src = Path(out_dir, "scene.tif") if from_file else r  # file: each rank decodes only its own windows
+    streams = encode_tiles_distributed(src, tiles, 5, d, encode_fn=oracle_encode_tiles)
     if rank == 0:
         blob = assemble_streaming(tiles, streams, r.shape, r.dtype, Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0),
                                   "EPSG:3857", 64)
-        Path(out_dir, f"w{world}.bin").write_bytes(blob)
+        Path(out_dir, f"w{world}{'f' if from_file else ''}.bin").write_bytes(blob)
     else:
         assert streams is None
     d.close()
@@ -71,6 +72,31 @@ def test_distributed_container_identical(tmp_path, world):
     ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, 5), r.shape, r.dtype,
                              Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0), "EPSG:3857", 64)
     assert (tmp_path / f"w{world}.bin").read_bytes() == ref
+
+
+def test_distributed_ranks_read_own_windows(tmp_path):
+    """World 2 from a GeoTIFF file: each rank decodes only its LPT tiles' windows into a rank-local
+    mosaic (read_rank_mosaic) and the container equals the single-process one."""
+    sys.path.insert(0, str(HERE))
+    from flac_raster.dist import read_rank_mosaic, shard
+    from flac_raster.geo import Affine
+    from flac_raster.streaming import assemble_streaming
+    from flac_raster.tiff import write_geotiff
+    from flac_raster.tiles import calculate_tiles
+    from oracle_tiles import oracle_encode_tiles
+
+    r = _raster()
+    write_geotiff(tmp_path / "scene.tif", r)
+    tiles = calculate_tiles(200, 333, 64)
+    mine = [tiles[i] for i in shard(tiles, 2, 1)]
+    mosaic, local = read_rank_mosaic(tmp_path / "scene.tif", mine)
+    assert mosaic.shape[1] == sum(t[2] for t in mine) and mosaic.nbytes < r.nbytes
+    for (r0, c0, h, w), (o, _, lh, lw) in zip(mine, local):
+        assert np.array_equal(mosaic[:, o:o + lh, :lw], r[:, r0:r0 + h, c0:c0 + w])
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), True), nprocs=2, join=True)
+    ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, 5), r.shape, r.dtype,
+                             Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0), "EPSG:3857", 64)
+    assert (tmp_path / "w2f.bin").read_bytes() == ref
 
 
 def test_shards_partition_tiles():
