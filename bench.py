@@ -674,8 +674,64 @@ def measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, dev_plan):
     tp = time.perf_counter() - t0
     res["pageable"] = {"value": round(my_px / tp / 1e6, 2), "ms": round(tp * 1e3, 2)}
     plan.close()
-    del host, out, hp, op
+    del out, hp, op
+    if os.environ.get("FRA_E2E_FILE", "1") != "0" and len(my_wins) == len(tiles(H, W, cfg["tile"])):
+        try:
+            res["e2e_file"] = measure_e2e_file(N, cfg, host, dev_plan, res["pcie_floor_ms"])
+        except Exception as e:  # reported, never fatal for the headline line
+            res["e2e_file"] = {"error": f"{type(e).__name__}: {e}"}
+    del host
     return res
+
+
+def measure_e2e_file(N, cfg, host, dev_plan, pcie_floor_ms):
+    """File -> container bytes in memory (cli.py:553-602): the scene written once as a
+    tiled deflate and once as a tiled LZW GeoTIFF (tile 512, predictor 2, native writer), then
+    ``encode_geotiff_streaming`` -- the decode of row band b+1 on a producer thread overlapped with the
+    H2D / kernels / D2H of band b (fra_plan_encode_host_progress) -- plus the container assembly.
+    Decode alone (the same threaded decoder into page-locked memory) is timed separately."""
+    from flac_raster.geo import Affine
+    from flac_raster.streaming import encode_geotiff_streaming, streaming_parts
+    from flac_raster.tiff import GeoTIFF, write_geotiff
+
+    ref = dev_plan.download()[1]
+    out = {"what": "tiled GeoTIFF file (page cache) -> decode || H2D || kernels || D2H -> container bytes "
+                   "in memory; decode_ms = the same threaded decode alone"}
+    tmpd = tempfile.mkdtemp(prefix="fra_e2e_", dir="/tmp")
+    try:
+        B, H, W = host.shape
+        for comp in ("deflate", "lzw"):
+            p = Path(tmpd) / f"scene_{comp}.tif"
+            write_geotiff(p, host, compression=comp, tile=512, predictor=2, level=6)
+            g = GeoTIFF(p)
+            dec = N.pinned_empty(host.shape, host.dtype)
+            t0 = time.perf_counter()
+            g.read_window_into(dec, 0, 0, H, W)
+            t_dec = time.perf_counter() - t0
+            g.close()
+            same_raster = bool(np.array_equal(dec, host))
+            del dec
+            encode_geotiff_streaming(p, cfg["tile"], cfg["level"])  # warm-up (plan pool, pinned pool)
+            best = None
+            for _ in range(2):
+                t0 = time.perf_counter()
+                tl, streams, shape, dtype, info = encode_geotiff_streaming(p, cfg["tile"], cfg["level"])
+                parts = streaming_parts(tl, streams, shape, dtype, Affine(*info.transform), info.crs, cfg["tile"])
+                te = time.perf_counter() - t0
+                best = te if best is None else min(best, te)
+            equal = b"".join(bytes(ts.body) for ts in streams) == ref
+            floor = max(t_dec * 1e3, pcie_floor_ms)
+            out[comp] = {"file_bytes": p.stat().st_size, "ms": round(best * 1e3, 2),
+                         "mpix_s": round(H * W / best / 1e6, 2), "decode_ms": round(t_dec * 1e3, 2),
+                         "decode_mpix_s": round(H * W / t_dec / 1e6, 2),
+                         "ratio_vs_max_decode_pcie": round(best * 1e3 / floor, 3),
+                         "bytes_equal_device_path": bool(equal), "decoded_raster_equal": same_raster,
+                         "container_bytes": int(sum(len(x) for x in parts))}
+            del streams, parts
+            p.unlink()
+    finally:
+        shutil.rmtree(tmpd, ignore_errors=True)
+    return out
 
 
 if __name__ == "__main__":

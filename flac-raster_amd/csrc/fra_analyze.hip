@@ -315,14 +315,30 @@ __device__ __forceinline__ uint32_t lpc_abs16(const int32_t* x, const int32_t* q
 // orders skipped) == oracle fg1/fg2.  Wave-uniform, every wave may run it.
 __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kMaxPart], const int8_t* mvalid, int P,
                                              int lane, int& g1, int& g2) {
-  uint64_t T[5];
+  uint64_t T[5], pv[5];
+  bool small = true;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
-    uint64_t v = lane < (1 << P) ? psum[k][lane] : 0ull;
-    v = up_add64<0>(v); v = up_add64<1>(v); v = up_add64<2>(v);
-    v = up_add64<3>(v); v = up_add64<4>(v); v = up_add64<5>(v);
-    T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    pv[k] = lane < (1 << P) ? psum[k][lane] : 0ull;
+    small = small && pv[k] < (1ull << 25);
+  }
+  if (__all(small)) {  // <= 64 partitions of < 2^25 each: the block totals fit 32 bits (1-instruction DPP adds)
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      uint32_t v = (uint32_t)pv[k];
+      v = up_add32<0>(v); v = up_add32<1>(v); v = up_add32<2>(v);
+      v = up_add32<3>(v); v = up_add32<4>(v); v = up_add32<5>(v);
+      T[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      uint64_t v = pv[k];
+      v = up_add64<0>(v); v = up_add64<1>(v); v = up_add64<2>(v);
+      v = up_add64<3>(v); v = up_add64<4>(v); v = up_add64<5>(v);
+      T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    }
   }
   // branch-free selects on uniform values (a branchy form let the compiler merge g1/g2 into a
   // dynamically indexed private array, i.e. scratch memory)
@@ -342,6 +358,76 @@ __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kM
   g2 = __builtin_amdgcn_readfirstlane(h2);
 }
 
+// porder_search (below) when every node sum is < 2^29: the same nodes, tree, tie rule and outputs in
+// 32-bit arithmetic (one-instruction DPP adds, rice_pick32)
+__device__ __forceinline__ void porder_search32(const unsigned long long* psum, uint32_t* node, int P, int pm, int n,
+                                                int o, int lane, uint32_t Sv, uint64_t& best_out, int& bp_out,
+                                                uint8_t* kout) {
+  (void)psum;
+  if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
+#define FRA_NODE_STEP32(S_)                                                        \
+  if (P > S_) {                                                                    \
+    Sv = up_add32<S_>(Sv);                                                         \
+    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
+      node[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = Sv;                         \
+  }
+  FRA_NODE_STEP32(0)
+  FRA_NODE_STEP32(1)
+  FRA_NODE_STEP32(2)
+  FRA_NODE_STEP32(3)
+  FRA_NODE_STEP32(4)
+  FRA_NODE_STEP32(5)
+#undef FRA_NODE_STEP32
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  uint32_t bits32 = 0;
+  bool big = false;
+  const int p = lane ? 31 - __clz(lane) : 0;
+  int kn = 0;
+  if (lane >= 1 && p <= P && p <= pm) {
+    const int j = lane - (1 << p);
+    rice_pick32((uint32_t)((n >> p) - (j == 0 ? o : 0)), node[lane], kn, bits32);
+    big = kn > 14;
+  }
+  const uint64_t bigm = __ballot(big);
+  uint32_t tot[7];
+  uint32_t v = bits32;
+  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
+  v += dpp32<DPP_SHR1, 0xF>(v);
+  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+  v += dpp32<DPP_SHR2, 0xF>(v);
+  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
+  v += dpp32<DPP_SHR4, 0xF>(v);
+  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  v += dpp32<DPP_SHR8, 0xF>(v);
+  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  v += dpp32<DPP_BC15, 0xA>(v);
+  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  tot[6] = 0;
+  bool big6 = false;
+  int k6 = 0;
+  if (P == 6 && pm == 6) {  // level 6: 64 nodes at node[64 + lane]
+    uint32_t b6;
+    rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), node[64 + lane], k6, b6);
+    tot[6] = wave_sum32(b6);
+    big6 = __any(k6 > 14);
+  }
+  uint64_t best = 0;
+  int bp = pm;
+  for (int q = pm; q >= 0; q--) {
+    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
+    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
+    if (q == pm || t <= best) { best = t; bp = q; }
+  }
+  best_out = best;
+  bp_out = bp;
+  if (kout) {
+    if (bp == 6) kout[lane] = (uint8_t)k6;
+    else if (lane >= (1 << bp) && lane < (2 << bp)) kout[lane - (1 << bp)] = (uint8_t)kn;
+  }
+}
+
 // Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at
 // lane 2^p + j (level P = 6 nodes in a second register), so each lane runs ONE Rice estimate and
 // the per-level totals come out of a single upper-lane DPP chain (level p's segment is the aligned
@@ -352,6 +438,12 @@ __device__ __forceinline__ void porder_search(const unsigned long long* psum, un
                                               uint8_t* kout = nullptr) {
   // node sums: finest sums S_j, then upper-lane group sums (leader lane of 2^s lanes = (j+1)2^s - 1)
   uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
+  if (__all(Sv < (1ull << 23))) {
+    // every node sum < 2^29 (<= 64 finest partitions of < 2^23): the whole search in 32-bit arithmetic
+    // (rice_pick32), bit-identical to the 64-bit form below; node sums kept as u32 in the same buffer
+    porder_search32(psum, reinterpret_cast<uint32_t*>(node), P, pm, n, o, lane, (uint32_t)Sv, best_out, bp_out, kout);
+    return;
+  }
   if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
 #define FRA_NODE_STEP(S_)                                                          \
   if (P > S_) {                                                                    \
@@ -452,7 +544,7 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 #define FRA_FASTLOAD 1  // full-frame LUT load path (load_lut_full)
 #endif
 #ifndef FRA_WAVES16
-#define FRA_WAVES16 5   // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
+#define FRA_WAVES16 6   // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
 #endif
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16)) k_analyze(JobArgs a, int src) {
@@ -502,7 +594,9 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVE
       if (FRA_FASTLOAD && lut && a.vec8 && a.off32 && n == kMaxBlock)
         done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
     }
+#ifndef FRA_ONLYFAST
     if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
+#endif
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -621,12 +715,6 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVE
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = fixfast && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
 
-  // apodization window coefficients of this thread's samples (+ MAXLAG lookahead), first window
-  float wcur[MAXLAG > 0 ? kChunk + MAXLAG : 1];
-  if constexpr (MAXLAG > 0) {
-    const float* win = a.win + (size_t)fr.win * a.nwin * a.blocksize;
-    load_window<MAXLAG>(win, t * kChunk, n, wcur);
-  }
   // partial windows are zero outside their segment (host-computed extent [lo, hi)): a wave whose
   // samples + lookahead [1024 wv, 1024 wv + 1024 + MAXLAG) miss it would only sum exact products of
   // zeros, i.e. every chunk partial is +0.0 -- it skips the window and stores those zeros directly
@@ -643,11 +731,15 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVE
       // 3.1 autocorrelation of every window: windowed samples -> chunk partials -> wave
       // reduce-scatter -> red[wi][wave][lag].  Window 0 is peeled so its prefetched coefficients die
       // at their first use.
-      auto window_acf = [&](const int wi, const float (&wcoef)[kChunk + MAXLAG], const bool act) {
+      auto window_acf = [&](const int wi, const bool act) {
         if (!act) {
           if (lane <= MAXLAG) S.red[wi][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
           return;
         }
+        // coefficients loaded here, not prefetched before the FIXED sums: a prefetch kept 16 + MAXLAG
+        // registers live through them and pushed the 7-wave instance into scratch
+        float wcoef[kChunk + MAXLAG];
+        load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];
@@ -684,14 +776,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVE
         for (int l = 0; l <= MAXLAG; l++) acc[l] = (double)(pacc[l].x + pacc[l].y);
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi][wv], lane);
       };
-      window_acf(0, wcur, wave_active(0));
-      for (int wi = 1; wi < a.nwin; wi++) {
-        float wl[kChunk + MAXLAG];
-        const bool act = wave_active(wi);
-        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
-        if (act) load_window<MAXLAG>(win, i0, n, wl);
-        window_acf(wi, wl, act);
-      }
+      for (int wi = 0; wi < a.nwin; wi++) window_acf(wi, wave_active(wi));
       __syncthreads();
       FRA_STAMP(3)
       FRA_STOP(8)
@@ -756,7 +841,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVE
           o = (int)__builtin_ctz(rowbits);
           double lpo[MAXLAG];
 #pragma unroll
-          for (int j = 0; j < MAXLAG; j++) lpo[j] = j < o ? S.lp[ws][lp_row(o - 1) + j] : 0.0;
+          for (int j = 0; j < MAXLAG; j++) lpo[j] = j < o ? -S.lp[ws][lp_row(o - 1) + j] : 0.0;  // lp = -lpc
           ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
         }
         if (gon && lo == 0) {

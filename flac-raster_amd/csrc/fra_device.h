@@ -552,7 +552,11 @@ __device__ __forceinline__ uint32_t zz32(int32_t r) { return ((uint32_t)r << 1) 
 // v_sad_u32.  The estimate sums are 2 * sum |r|.
 constexpr uint32_t kBias = 0x80000000u;
 __device__ __forceinline__ uint32_t sad_acc(uint32_t ab, uint32_t bb, uint32_t acc) {
-  return (ab > bb ? ab - bb : bb - ab) + acc;
+  // forced: from the select form the compiler emitted v_sub_co + v_cndmask + v_add3 (and an s_nop for the
+  // vcc hazard) wherever one operand was the constant bias -- three VALU instructions instead of one
+  uint32_t d;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(ab), "v"(bb), "v"(acc));
+  return d;
 }
 __device__ __forceinline__ uint64_t abs2_64(int64_t r) { return 2 * (uint64_t)(r < 0 ? -r : r); }
 __device__ __forceinline__ int bitlen64(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
@@ -573,6 +577,29 @@ __device__ __forceinline__ void rice_pick(uint64_t n, uint64_t S, int& k_out, ui
   int bk = lo;
   for (int k = lo + 1; k <= hi; k++) {
     const uint64_t e = rice_est2(n, S, k);
+    if (e < best) { best = e; bk = k; }
+  }
+  k_out = bk;
+  bits_out = best;
+}
+
+// the same pick in 32-bit arithmetic, valid (bit-identical) whenever S < 2^29 and n < 2^13: then
+// kc <= bitlen(S) - bitlen(n) + 1, so n * 2^k < 2^31 for every candidate k <= kc + 1, 2S < 2^30, and no
+// intermediate wraps; n * (2^k - 1) as (n << k) - n, n * (k + 1) on the 24-bit multiplier
+__device__ __forceinline__ void rice_pick32(uint32_t n, uint32_t S, int& k_out, uint32_t& bits_out) {
+  const int a = S ? 32 - __clz((int)S) : 0, b = n ? 32 - __clz((int)n) : 0;
+  int kc = a > b ? a - b : 0;
+  if (S >= (n << kc)) kc++;
+  const int lo = kc - 2 < 0 ? 0 : kc - 2, hi = kc + 1 > 30 ? 30 : kc + 1;
+  auto est = [&](int k) -> uint32_t {
+    const uint32_t l = (n << k) - n;
+    const uint32_t tail = (2 * S > l) ? ((2 * S - l) >> (k + 1)) : 0u;
+    return __umul24(n, (uint32_t)(k + 1)) + tail;
+  };
+  uint32_t best = est(lo);
+  int bk = lo;
+  for (int k = lo + 1; k <= hi; k++) {
+    const uint32_t e = est(k);
     if (e < best) { best = e; bk = k; }
   }
   k_out = bk;
@@ -659,9 +686,9 @@ __device__ inline int levinson_wave(const double (&ac)[MAXLAG + 1], int max_orde
       }
       if (i & 1) lpc[i >> 1] = lpc[i >> 1] + lpc[i >> 1] * r;
       err = err * (1.0 - r * r);
-      if (writer) {
+      if (writer) {  // rows stored as lpc (the reader negates the one row it quantises)
 #pragma unroll
-        for (int j = 0; j <= i; j++) lp[lp_row(i) + j] = -lpc[j];
+        for (int j = 0; j <= i; j++) lp[lp_row(i) + j] = lpc[j];
       }
       errv[i] = err;
       if (!(err > 0.0)) {

@@ -91,7 +91,7 @@ EXPORTS = [
     "fra_device_free", "fra_memcpy_d2h", "fra_memcpy_h2d", "fra_plan_frame_offsets", "fra_normalize",
     "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
     "fra_host_register", "fra_host_unregister", "fra_tiff_decode", "fra_plan_set_first_frame",
-    "fra_plan_flags",
+    "fra_plan_flags", "fra_plan_encode_host_progress", "fra_tiff_compress_bound", "fra_tiff_compress",
 ]
 
 
@@ -147,6 +147,10 @@ def load():
         L.fra_host_register.argtypes = [vp, u64]
         L.fra_host_unregister.argtypes = [vp]
         L.fra_tiff_decode.argtypes = [vp, u64, C.POINTER(TiffLayout), C.POINTER(TiffChunk), i32, vp, i32]
+        L.fra_plan_encode_host_progress.argtypes = [vp, vp, vp, u64, C.POINTER(u64), vp]
+        L.fra_tiff_compress_bound.argtypes = [i32, u64]
+        L.fra_tiff_compress_bound.restype = u64
+        L.fra_tiff_compress.argtypes = [i32, i32, vp, u64, i32, vp, u64, C.POINTER(u64), i32]
         _lib = L
         return L
 
@@ -366,7 +370,7 @@ class Plan:
         _check(load().fra_plan_set_first_frame(self.h, int(n)))
 
     def flags(self) -> int:
-        """``FRA_PLAN_*`` bits: 1 direct write (subframes placed by k_analyze), 2 cross-execute pipelined."""
+        """``FRA_PLAN_*`` bits: 2 cross-execute pipelined (1, direct write, is never set since r03)."""
         f = C.c_int32()
         _check(load().fra_plan_flags(self.h, C.byref(f)))
         return f.value
@@ -387,6 +391,22 @@ class Plan:
         self._keep = raster
         rc = load().fra_plan_encode_host(self.h, C.c_void_p(raster.ctypes.data), C.c_void_p(out.ctypes.data),
                                          out.nbytes, C.byref(total))
+        if rc == E_SPACE:
+            raise OutputTooSmall(total.value)
+        _check(rc)
+        return total.value
+
+    def encode_host_progress(self, raster: np.ndarray, out: np.ndarray, rows_ready: np.ndarray) -> int:
+        """:meth:`encode_host` over a raster still being produced (``fra_plan_encode_host_progress``): a
+        producer thread fills ``raster`` top to bottom and publishes the rows done in ``rows_ready[0]``
+        (int64; -1 = failed); each row band's H2D copy waits for its rows."""
+        if rows_ready.dtype != np.int64 or rows_ready.size < 1:
+            raise ValueError("rows_ready must be an int64 array of >= 1 element")
+        total = C.c_uint64()
+        self._keep = raster
+        rc = load().fra_plan_encode_host_progress(self.h, C.c_void_p(raster.ctypes.data),
+                                                  C.c_void_p(out.ctypes.data), out.nbytes, C.byref(total),
+                                                  C.c_void_p(rows_ready.ctypes.data))
         if rc == E_SPACE:
             raise OutputTooSmall(total.value)
         _check(rc)
@@ -476,12 +496,15 @@ def _element_strides(a: np.ndarray) -> Tuple[int, int, int]:
 
 
 def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize: int = 4096, norm: int = 16,
-                          sample_rate: int = 0, device: int = 0, pinned: bool = True):
+                          sample_rate: int = 0, device: int = 0, pinned: bool = True,
+                          rows_ready: Optional[np.ndarray] = None):
     """Encode windows of a band-planar host raster ``(B, H, W)`` (any non-negative strides, e.g. a row
     band view of a larger raster) through the pipelined host path (``fra_plan_encode_host``).
 
     Returns ``(infos, frames)``: ``frames`` is a uint8 array (page-locked unless ``pinned=False``) with
     every window's FLAC frames concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.
+    ``rows_ready``: the raster is still being filled by a producer thread that publishes the rows done
+    in ``rows_ready[0]`` (``fra_plan_encode_host_progress``).
     """
     a = np.asarray(raster)
     if a.ndim == 2:
@@ -496,7 +519,7 @@ def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize
     try:
         cap, _ = plan.capacity()
         out = pinned_empty(cap, np.uint8) if pinned else np.empty(cap, np.uint8)
-        total = plan.encode_host(a, out)
+        total = plan.encode_host(a, out) if rows_ready is None else plan.encode_host_progress(a, out, rows_ready)
         infos, _ = plan.result()
         return infos, out[:total]
     finally:
@@ -570,3 +593,19 @@ def decode(data: bytes, concat: bool = False) -> Tuple[np.ndarray, Decoded]:
     finally:
         L.fra_free(ptr)
     return out.reshape(-1, info.channels), info
+
+
+def tiff_compress(compression: int, chunks: np.ndarray, level: int = 6, threads: int = 0):
+    """Compress equal-size raw TIFF chunks (``chunks``: uint8 array (nchunks, chunk_bytes), file layout,
+    predictor already applied) with LZW (5) or deflate (8) on the native thread pool
+    (``fra_tiff_compress``).  Returns a list of ``bytes``, one per chunk."""
+    chunks = np.ascontiguousarray(chunks, dtype=np.uint8)
+    n, cb = chunks.shape
+    L = load()
+    stride = int(L.fra_tiff_compress_bound(int(compression), int(cb)))
+    dst = np.empty(max(1, n) * stride, np.uint8)
+    sizes = np.zeros(max(1, n), np.uint64)
+    _check(L.fra_tiff_compress(int(compression), int(level), C.c_void_p(chunks.ctypes.data), int(cb), int(n),
+                               C.c_void_p(dst.ctypes.data), stride, sizes.ctypes.data_as(C.POINTER(C.c_uint64)),
+                               int(threads)))
+    return [dst[i * stride:i * stride + int(sizes[i])].tobytes() for i in range(n)]

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import json
 import struct
+import threading
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -84,19 +85,64 @@ def build_streaming(raster: np.ndarray, transform: Affine, crs: Optional[str], t
     return assemble_streaming(tiles, streams, a.shape, a.dtype, transform, crs, tile_size)
 
 
+def decode_while_encoding(g: GeoTIFF, tile_size: int):
+    """Start decoding a GeoTIFF into page-locked memory on a producer thread, top to bottom in row bands
+    (one tile row, rounded up to whole TIFF strips/tiles): returns ``(raster, rows_ready, thread)``;
+    ``rows_ready[0]`` = rows decoded so far (-1 on failure).  The encoder's host pipeline copies a band
+    H2D as soon as its rows are published (``fra_plan_encode_host_progress``), so the decode of band b+1
+    overlaps the PCIe copies and kernels of band b."""
+    from .tiff import _alloc
+
+    info = g.info
+    raster = _alloc((info.count, info.height, info.width), info.dtype, True)
+    rows_ready = np.zeros(1, np.int64)
+    step = max(tile_size, g.ch)
+    step = ((step + g.ch - 1) // g.ch) * g.ch if g.ch < info.height else info.height
+    errors: list = []
+
+    def run():
+        try:
+            for r0 in range(0, info.height, step):
+                r1 = min(info.height, r0 + step)
+                g.read_window_into(raster[:, r0:r1, :], r0, 0, r1 - r0, info.width)
+                rows_ready[0] = r1
+        except BaseException as e:  # reported to the encoder (rows_ready = -1) and re-raised by the caller
+            errors.append(e)
+            rows_ready[0] = -1
+
+    th = threading.Thread(target=run, name="geotiff-decode", daemon=True)
+    th.errors = errors  # type: ignore[attr-defined]
+    th.start()
+    return raster, rows_ready, th
+
+
+def encode_geotiff_streaming(input_path: Path, tile_size: int = 512, compression_level: int = 5,
+                             devices: Optional[Sequence[int]] = None):
+    """GeoTIFF file -> (tiles, streams, raster info): decode and encode overlapped (decode_while_encoding)."""
+    g = GeoTIFF(input_path)
+    raster, rows_ready, th = decode_while_encoding(g, tile_size)
+    try:
+        tiles = calculate_tiles(raster.shape[1], raster.shape[2], tile_size)
+        try:
+            streams = encode_tiles(raster, tiles, compression_level, devices, rows_ready=rows_ready, producer=th)
+        finally:
+            th.join()
+        if th.errors:  # type: ignore[attr-defined]
+            raise th.errors[0]  # type: ignore[attr-defined]
+        return tiles, streams, raster.shape, raster.dtype, g.info
+    finally:
+        g.close()
+
+
 def create_streaming_flac(input_path: Path, output_path: Path, tile_size: int = 512, compression_level: int = 5,
                           devices: Optional[Sequence[int]] = None) -> Dict:
     """Write the streaming container for a GeoTIFF; returns the index.
 
-    The raster is decoded straight into page-locked memory (``GeoTIFF.read(pinned=True)``), encoded by
-    the pipelined host path (row bands H2D while earlier bands are analysed, frames D2H per band) and
-    the container is written from zero-copy views of the page-locked frames."""
-    g = GeoTIFF(input_path)
-    raster = g.read(pinned=True)
-    tiles = calculate_tiles(raster.shape[1], raster.shape[2], tile_size)
-    streams = encode_tiles(raster, tiles, compression_level, devices)
-    parts = streaming_parts(tiles, streams, raster.shape, raster.dtype, Affine(*g.info.transform), g.info.crs,
-                            tile_size)
+    The raster is decoded into page-locked memory by a producer thread, row band by row band, while the
+    pipelined host path encodes the bands already decoded (H2D, kernels and D2H of band b overlap the
+    decode of band b+1); the container is written from zero-copy views of the page-locked frames."""
+    tiles, streams, shape, dtype, info = encode_geotiff_streaming(input_path, tile_size, compression_level, devices)
+    parts = streaming_parts(tiles, streams, shape, dtype, Affine(*info.transform), info.crs, tile_size)
     with open(output_path, "wb") as f:
         for p in parts:
             f.write(p)

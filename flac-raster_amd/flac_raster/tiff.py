@@ -233,7 +233,7 @@ class GeoTIFF:
                            col_off, height, width, 0, out.strides[0] // es, out.strides[1] // es)
         src = np.frombuffer(self._buf, dtype=np.uint8)
         N._check(N.load().fra_tiff_decode(src.ctypes.data_as(C.c_void_p), len(self._buf), C.byref(lay), arr,
-                                          len(chunks), out.ctypes.data_as(C.c_void_p), threads))
+                                          len(chunks), out.ctypes.data_as(C.c_void_p), threads or _threads()))
         del src
         return out
 
@@ -257,6 +257,15 @@ class GeoTIFF:
         return self.read_window_into(out, row_off, col_off, height, width)
 
 
+def _threads() -> int:
+    """Decoder threads: the process's CPU share (OMP_NUM_THREADS, set to the share on the GPU boxes), else
+    at most 16 -- os.cpu_count() reports the whole machine there."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def _alloc(shape, dtype, pinned: bool) -> np.ndarray:
     if pinned:
         from . import _native as N
@@ -270,28 +279,15 @@ def read_geotiff(path, pinned: bool = False):
     return g.read(pinned=pinned), g.info
 
 
-def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = None, nodata=None):
-    """Write an uncompressed, pixel-interleaved, single-strip-per-row-block little-endian GeoTIFF."""
-    data = np.asarray(data)
-    if data.ndim == 2:
-        data = data[None]
-    S, H, W = data.shape
-    dt = data.dtype
+def _geo_entries(S, H, W, dt, transform, crs, nodata):
     fmt = 3 if dt.kind == "f" else (2 if dt.kind == "i" else 1)
     bits = dt.itemsize * 8
-    pix = np.ascontiguousarray(np.moveaxis(data, 0, 2)).astype(dt.newbyteorder("<"), copy=False)
-    rows_per_strip = max(1, min(H, (1 << 16) // max(1, W * S * dt.itemsize)))
-    strips = [pix[r:r + rows_per_strip].tobytes() for r in range(0, H, rows_per_strip)]
     entries = []  # (tag, type, values)
     entries.append((256, 3 if W < 65536 else 4, [W]))
     entries.append((257, 3 if H < 65536 else 4, [H]))
     entries.append((258, 3, [bits] * S))
-    entries.append((259, 3, [1]))
     entries.append((262, 3, [2 if S == 3 and dt == np.uint8 else 1]))
-    entries.append((273, 4, [0] * len(strips)))
     entries.append((277, 3, [S]))
-    entries.append((278, 4, [rows_per_strip]))
-    entries.append((279, 4, [len(s) for s in strips]))
     entries.append((284, 3, [1]))
     entries.append((339, 3, [fmt] * S))
     if transform is not None:
@@ -309,8 +305,12 @@ def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = N
         entries.append((34735, 3, keys))
     if nodata is not None:
         entries.append((42113, 2, (str(nodata) + "\x00").encode("latin-1")))
-    entries.sort(key=lambda x: x[0])
-    # layout: header(8) | IFD | external values | strips
+    return entries
+
+
+def _write_tiff(path, entries, chunks, offsets_tag: int):
+    """Classic little-endian TIFF: header | IFD | external tag values | chunks (offsets patched)."""
+    entries = sorted(entries, key=lambda x: x[0])
     n = len(entries)
     ifd_size = 2 + 12 * n + 4
     ext = bytearray()
@@ -325,7 +325,6 @@ def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = N
             raw = struct.pack("<" + fmtmap[typ] * len(vals), *vals)
             cnt = len(vals)
         packed.append([tag, typ, cnt, raw])
-    # strip offsets need final positions: compute external area first with placeholder offsets
     for it in packed:
         if len(it[3]) > 4:
             it.append(ext_base + len(ext))
@@ -334,24 +333,74 @@ def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = N
                 ext += b"\x00"
         else:
             it.append(None)
-    strip_base = ext_base + len(ext)
-    offsets, pos = [], strip_base
-    for s in strips:
+    offsets, pos = [], ext_base + len(ext)
+    for c in chunks:
         offsets.append(pos)
-        pos += len(s)
-    for it in packed:  # patch StripOffsets
-        if it[0] == 273:
+        pos += len(c)
+    if pos >= (1 << 32):
+        raise ValueError("file larger than 4 GiB needs BigTIFF, which this writer does not produce")
+    for it in packed:  # patch the chunk offsets
+        if it[0] == offsets_tag:
             raw = struct.pack("<" + "I" * len(offsets), *offsets)
             it[3] = raw
             if it[4] is not None:
                 ext[it[4] - ext_base:it[4] - ext_base + len(raw)] = raw
-    out = bytearray(b"II*\x00" + struct.pack("<I", 8))
-    out += struct.pack("<H", n)
+    head = bytearray(b"II*\x00" + struct.pack("<I", 8))
+    head += struct.pack("<H", n)
     for tag, typ, cnt, raw, loc in packed:
-        out += struct.pack("<HHI", tag, typ, cnt)
-        out += struct.pack("<I", loc) if loc is not None else raw.ljust(4, b"\x00")
-    out += struct.pack("<I", 0)
-    out += ext
-    for s in strips:
-        out += s
-    Path(path).write_bytes(bytes(out))
+        head += struct.pack("<HHI", tag, typ, cnt)
+        head += struct.pack("<I", loc) if loc is not None else raw.ljust(4, b"\x00")
+    head += struct.pack("<I", 0)
+    head += ext
+    with open(path, "wb") as f:
+        f.write(head)
+        for c in chunks:
+            f.write(c)
+
+
+def write_geotiff(path, data: np.ndarray, transform=None, crs: Optional[str] = None, nodata=None,
+                  compression: Optional[str] = None, tile: Optional[int] = None, predictor: int = 1,
+                  level: int = 6):
+    """Write a pixel-interleaved little-endian GeoTIFF: uncompressed strips by default (the layout the
+    tests' fixtures use), or ``tile`` x ``tile`` tiles compressed with ``compression`` = "lzw" / "deflate"
+    (native thread pool, ``fra_tiff_compress``) and ``predictor`` 2 (horizontal differencing, integer
+    samples) -- the tiled GeoTIFFs rasterio writes for the tile files of ``cli.py:577-591``."""
+    data = np.asarray(data)
+    if data.ndim == 2:
+        data = data[None]
+    S, H, W = data.shape
+    dt = data.dtype
+    entries = _geo_entries(S, H, W, dt, transform, crs, nodata)
+    if compression is None and tile is None:
+        pix = np.ascontiguousarray(np.moveaxis(data, 0, 2)).astype(dt.newbyteorder("<"), copy=False)
+        rows_per_strip = max(1, min(H, (1 << 16) // max(1, W * S * dt.itemsize)))
+        strips = [pix[r:r + rows_per_strip].tobytes() for r in range(0, H, rows_per_strip)]
+        entries += [(259, 3, [1]), (273, 4, [0] * len(strips)), (278, 4, [rows_per_strip]),
+                    (279, 4, [len(x) for x in strips])]
+        _write_tiff(path, entries, strips, 273)
+        return
+    comp = {None: 1, "none": 1, "lzw": 5, "deflate": 8}[compression]
+    T = int(tile or 256)
+    if T % 16:
+        raise ValueError("TIFF tile size must be a multiple of 16")
+    if predictor not in (1, 2) or (predictor == 2 and dt.kind == "f"):
+        raise ValueError("predictor 1, or 2 on integer samples")
+    nx, ny = (W + T - 1) // T, (H + T - 1) // T
+    pix = np.zeros((ny * T, nx * T, S), dt.newbyteorder("<"))
+    pix[:H, :W] = np.moveaxis(data, 0, 2)
+    tiles = pix.reshape(ny, T, nx, T, S).transpose(0, 2, 1, 3, 4)  # (ny, nx, T rows, T cols, S)
+    if predictor == 2:  # horizontal differencing per tile row, stride = samples per pixel (modular)
+        u = tiles.view(np.dtype(f"<u{dt.itemsize}"))
+        d = u.copy()
+        d[:, :, :, 1:, :] = u[:, :, :, 1:, :] - u[:, :, :, :-1, :]
+        tiles = d
+    raw = np.ascontiguousarray(tiles).reshape(ny * nx, T * T * S).view(np.uint8)
+    if comp == 1:
+        chunks = [raw[i].tobytes() for i in range(raw.shape[0])]
+    else:
+        from . import _native as N
+
+        chunks = N.tiff_compress(comp, raw, level=level)
+    entries += [(259, 3, [comp]), (317, 3, [predictor]), (322, 3, [T]), (323, 3, [T]),
+                (324, 4, [0] * len(chunks)), (325, 4, [len(x) for x in chunks])]
+    _write_tiff(path, entries, chunks, 324)

@@ -97,14 +97,16 @@ def norm_bits(dtype) -> int:
 
 
 def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int, device: int,
-                  norm: int, out: list, errors: list, slot: int):
+                  norm: int, out: list, errors: list, slot: int, rows_ready=None):
     try:
         r0 = min(t[0] for t in tiles)
         r1 = max(t[0] + t[2] for t in tiles)
         sub = raster[:, r0:r1, :]  # a view: the plan copies only these rows, band by band
         wins = [(t[0] - r0, t[1], t[2], t[3]) for t in tiles]
+        if rows_ready is not None and r0 != 0:
+            raise ValueError("rows_ready needs the group to start at raster row 0")
         infos, frames = _native.encode_windows_buffer(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
-                                                      device=device)
+                                                      device=device, rows_ready=rows_ready)
         res = []
         mv = memoryview(frames)
         for inf in infos:
@@ -117,11 +119,14 @@ def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]]
 
 
 def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,
-                 devices: Optional[Sequence[int]] = None) -> List[TileStream]:
+                 devices: Optional[Sequence[int]] = None, rows_ready=None,
+                 producer: Optional[threading.Thread] = None) -> List[TileStream]:
     """Encode every tile of a band-planar ``(B, H, W)`` raster as its own FLAC stream on the GPU(s).
 
     Each stream equals what ``normalize_to_audio`` + ``pyflac.StreamEncoder(blocksize=4096)``
     produce for ``raster[:, r:r+h, c:c+w]`` interleaved pixel-major (``cli.py:557-597``).
+    ``rows_ready`` / ``producer``: the raster is still being decoded by ``producer``, which publishes the
+    rows done in ``rows_ready[0]``; one device encodes as the rows land, several wait for the producer.
     """
     a = np.asarray(raster)
     if a.ndim == 2:
@@ -137,8 +142,14 @@ def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]],
     runs = split_contiguous([t[2] * t[3] for t in tiles], len(devs))
     out: list = [None] * len(runs)
     errors: list = []
+    if rows_ready is not None and (len(runs) > 1 or min(t[0] for t in tiles) != 0):
+        if producer is not None:
+            producer.join()
+        if rows_ready[0] < 0:
+            raise RuntimeError("raster decode failed")
+        rows_ready = None
     if len(runs) == 1:
-        _encode_group(a, tiles, level, devs[0], norm, out, errors, 0)
+        _encode_group(a, tiles, level, devs[0], norm, out, errors, 0, rows_ready)
     else:
         th = [threading.Thread(target=_encode_group, args=(a, tiles[s:e], level, devs[k], norm, out, errors, k))
               for k, (s, e) in enumerate(runs)]

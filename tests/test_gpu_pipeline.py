@@ -96,6 +96,43 @@ def test_compressed_geotiff_to_streaming_container(tmp_path, compression, predic
     assert out.read_bytes() == ref
 
 
+@pytest.mark.parametrize("compression,tile", [("deflate", 256), ("lzw", 512)])
+def test_native_tiled_geotiff_decode_overlapped_with_encode(tmp_path, compression, tile):
+    """4-band tiled GeoTIFF from the native writer (predictor 2): create_streaming_flac decodes it on a
+    producer thread while the host pipeline encodes the rows already published
+    (fra_plan_encode_host_progress) -- the container equals the oracle's."""
+    from flac_raster.tiff import write_geotiff
+
+    r = synth_window(4, 9, 4, 1500, 1200).astype(np.uint16)
+    p = tmp_path / "in.tif"
+    write_geotiff(p, r, compression=compression, tile=256, predictor=2)
+    out = tmp_path / "s.flac"
+    create_streaming_flac(p, out, tile, 5)
+    tiles = calculate_tiles(1500, 1200, tile)
+    ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, 5), r.shape, r.dtype,
+                             Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0), None, tile)
+    assert out.read_bytes() == ref
+
+
+def test_corrupt_geotiff_fails_cleanly_while_encoding(tmp_path):
+    """A chunk that fails to decode mid-file: the producer publishes -1, the host pipeline stops waiting
+    and reports the error (no hang, no partial container)."""
+    from flac_raster.tiff import GeoTIFF, write_geotiff
+
+    r = synth_window(4, 9, 1, 2048, 1024).astype(np.uint16)
+    p = tmp_path / "bad.tif"
+    write_geotiff(p, r, compression="deflate", tile=256, predictor=2)
+    g = GeoTIFF(p)
+    off = int(g._offs[len(g._offs) - 3])
+    g.close()
+    raw = bytearray(p.read_bytes())
+    raw[off:off + 64] = b"\xff" * 64  # not a deflate stream any more
+    p.write_bytes(bytes(raw))
+    with pytest.raises(Exception):
+        create_streaming_flac(p, tmp_path / "x.flac", 512, 5)
+    assert not (tmp_path / "x.flac").exists()
+
+
 def test_pinned_pool_reuse():
     a = N.pinned_empty(1 << 20, np.uint8)
     p = a.ctypes.data

@@ -248,3 +248,38 @@ def test_spec_writer_cross_checked_by_pillow(tmp_path, compression, pred):
     write_tiff(f, a, tile=(16, 16), compression=compression, predictor=pred)
     assert np.array_equal(np.asarray(PIL.open(f)), a[0])
     assert np.array_equal(GeoTIFF(f).read(), a)
+
+
+@pytest.mark.parametrize("compression", ["lzw", "deflate"])
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int16, np.float32])
+@pytest.mark.parametrize("pred", [1, 2])
+def test_native_tile_writer_round_trip_and_pillow(tmp_path, compression, dtype, pred):
+    """write_geotiff(compression=, tile=, predictor=) -- the native LZW / deflate chunk encoder
+    (fra_tiff_compress) -- reads back bit-exactly through fra_tiff_decode, and Pillow (libtiff) decodes
+    the single-band files identically (independent LZW decoder: early change, Clear/EOI placement)."""
+    if dtype == np.float32 and pred == 2:
+        pytest.skip("predictor 2 is for integer samples")
+    from flac_raster.tiff import write_geotiff
+
+    rng = np.random.default_rng(11)
+    base = np.cumsum(rng.integers(-3, 4, size=(3, 300, 333)), axis=2)
+    a = (base - base.min()).astype(dtype) if dtype != np.float32 else (base * 0.5).astype(dtype)
+    f = tmp_path / "t.tif"
+    write_geotiff(f, a, compression=compression, tile=128, predictor=pred)
+    b, _ = read_geotiff(f)
+    assert b.dtype == a.dtype and np.array_equal(a, b)
+    if dtype in (np.uint8, np.uint16):
+        write_geotiff(f, a[:1], compression=compression, tile=64, predictor=pred)
+        assert np.array_equal(np.asarray(PIL.open(f)).astype(dtype), a[0])
+
+
+def test_native_lzw_table_resets(tmp_path):
+    """Incompressible and constant tiles: the LZW table fills and restarts (Clear at 4093 entries)."""
+    from flac_raster.tiff import write_geotiff
+
+    rng = np.random.default_rng(3)
+    for a in (rng.integers(0, 256, size=(1, 700, 700)).astype(np.uint8), np.zeros((1, 512, 512), np.uint8)):
+        f = tmp_path / "r.tif"
+        write_geotiff(f, a, compression="lzw", tile=512)
+        assert np.array_equal(read_geotiff(f)[0], a)
+        assert np.array_equal(np.asarray(PIL.open(f)), a[0])
