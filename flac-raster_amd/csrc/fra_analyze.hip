@@ -546,8 +546,18 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 #ifndef FRA_WAVES16
 #define FRA_WAVES16 6   // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
 #endif
+#ifndef FRA_ANA_SGPR
+// SGPR cap (0 = compiler default; in effect on the 16-bit lag <= 8 instances, the others keep 106).  A
+// SIMD holds 800 SGPRs, allocated per wave as ceil(n/16)*16 + 16 (MI355X_MICROARCH.md, workgroup
+// dispatch): at the default 106 six analysis waves take 768 and no background wave (k_minmax_vec,
+// k_assemble_bg of the pipelined execute) fits beside them; at <= 94 they take 672 (the compiler keeps
+// the excess in VGPR lanes, still 80 VGPRs).  Off by default: the co-resident background assembly it
+// enables was slower on 16-bit plans and the cap costs the analysis ~1 %
+#define FRA_ANA_SGPR 0
+#endif
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16)) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16))
+__attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the

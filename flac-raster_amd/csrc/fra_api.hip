@@ -34,7 +34,7 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
-hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
+hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
                                 hipStream_t s, unsigned long long* host_mirror = nullptr);
@@ -124,7 +124,7 @@ struct fra_plan {
   unsigned long long* d_gbase_mirror = nullptr;  // its device address
   // cross-execute pipelining (FRA_PIPE, default on when a second buffer set fits in a third of the free
   // device memory, single frame group): execute k analyses into buffer set k % 2 on the plan's stream
-  // while k_assemble of execute k-1 (reading the other set) runs on the pack stream
+  // while the frame-size chain + assembly of execute k-1 (reading the other set) run on the pack stream
   bool pipe = false;
   int cur = 0;  // buffer set of the last execute
   SfDesc* sf2[2] = {};
@@ -136,8 +136,11 @@ struct fra_plan {
   hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
   bool pack_pending[2] = {false, false};
   // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
-  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set): k_minmax_vec
-  // fits the 32 VGPRs per SIMD that six k_analyze workgroups leave free, so it co-resides
+  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Whether a
+  // background workgroup co-resides with the analysis or takes an analysis workgroup's place depends on
+  // what the analysis leaves per SIMD: 16-bit plans (6 workgroups/CU) 32 VGPRs and 32 of 800 SGPRs (none
+  // fits), 32-bps plans (4/CU) 96 VGPRs, 288 SGPRs and 12.6 KiB of LDS per CU (k_minmax_vec and
+  // k_assemble_bg fit)
   NormDev* norm2[2] = {};
   int32_t* lut2[2] = {};
   hipStream_t nstream = nullptr;
@@ -694,6 +697,14 @@ static void use_buffers(fra_plan* p, int b) {
   p->args.norm = p->d_norm; p->args.lut = p->d_lut;
   p->cur = b;
 }
+// the pipelined execute's assembly kernel: k_assemble_bg (<= 32 VGPRs, one workgroup per CU) on 32-bps
+// plans, whose four analysis workgroups per CU leave room for it; k_assemble on 16-bit plans, where the
+// background form did not fit beside six analysis workgroups (SGPRs) and, made to fit (FRA_ANA_SGPR=94),
+// was slower than the per-frame grid (r03 v7/v8).  FRA_PIPE_ASM=0 / 1 forces k_assemble / k_assemble_bg.
+static bool pipe_asm_bg(const fra_plan* p) {
+  static const int m = getenv("FRA_PIPE_ASM") ? atoi(getenv("FRA_PIPE_ASM")) : -1;
+  return m < 0 ? p->b32 : m == 1;
+}
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
   if (!p->pipe) return FRA_OK;
@@ -827,6 +838,18 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st));
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
+  // pipelined execute: the frame-size chain (k_frame_bytes, scan, k_group_offsets) only feeds this
+  // execute's assembly, so it goes onto the pack stream with it and the plan's stream proceeds straight to
+  // the next execute's analysis (FRA_CHAIN_BG=0: the chain stays on the plan's stream)
+  static const bool chain_bg = !(getenv("FRA_CHAIN_BG") && atoi(getenv("FRA_CHAIN_BG")) == 0);
+  // background form of k_assemble (<= 32 VGPRs, ~one workgroup per CU) beside the next execute's analysis
+  const int bg_blocks = (pack_st && pipe_asm_bg(p)) ? p->ncu : 0;
+  if (pack_st && chain_bg && !ev_prev && !ev_pub && !host_mirror) {
+    HIPCHK(hipEventRecord(ev_scan, st));
+    HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
+    st = pack_st;
+    pack_st = nullptr;
+  }
   HIPCHK(launch_frame_bytes(ga, st));
   if (nf > 0) {
     size_t tb = p->scan_stride;
@@ -841,9 +864,9 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   if (pack_st) {  // assembly on the pack stream once this group's offsets exist
     HIPCHK(hipEventRecord(ev_scan, st));
     HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
-    HIPCHK(launch_assemble(ga, pack_st));
+    HIPCHK(launch_assemble(ga, pack_st, bg_blocks));
   } else {
-    HIPCHK(launch_assemble(ga, st));
+    HIPCHK(launch_assemble(ga, st, bg_blocks));
   }
   return FRA_OK;
 }

@@ -189,3 +189,54 @@ def test_cross_execute_pipelining_buffers():
             plan.close()
     finally:
         ctx.free(dev)
+
+
+@pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm", [
+    (4, 4, 4500, 4500, 1024, np.uint16, 5, 16),    # 4 channels, ragged edge tiles (k_analyze<16-bit, lag 8>)
+    (4, 2, 4500, 4096, 1000, np.uint16, 5, 16),    # 2 channels: mid-side slot map, odd tile width
+    (3, 1, 4096, 4096, 512, np.int16, 8, 16),      # lag-12 16-bit instance
+    (5, 2, 4096, 4096, 512, np.float32, 8, 24),    # 32-bps
+])
+def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level, norm):
+    """Pipelined executes run the frame-size chain and the assembly of execute k on the pack stream beside
+    execute k+1's analysis (k_assemble_bg on 32-bps plans, k_assemble on 16-bit ones).  The output of
+    execute 2, written into an output buffer poisoned after execute 1 and read after a device-wide barrier,
+    must be byte-identical to the serial (timing-mode) execute's; so must the plan's own download; and
+    sampled tiles must equal the oracle's frames."""
+    import torch  # device-wide barrier (hipDeviceSynchronize) independent of the plan's own sync
+
+    r = synth_window(kind, 91, bands, H, W).astype(dtype, copy=False)
+    wins = calculate_tiles(H, W, tile)
+    ctx = N.default_context(0)
+    dev = ctx.alloc(r.nbytes)
+    try:
+        ctx.h2d(dev, r)
+        plan = N.Plan(ctx, dev, True, r.dtype, bands, (H * W, W, 1), wins, level, 4096, norm)
+        try:
+            assert plan.flags() & 2, "plan too small for the pipelined execute (FRA_PLAN_PIPELINED)"
+            out_ptr, out_cap = plan.device_output()
+            plan.enable_timing(True)
+            plan.execute()
+            plan.sync()
+            infos_s, serial = plan.download()
+            plan.enable_timing(False)
+            plan.execute()  # execute 1
+            torch.cuda.synchronize()
+            ctx.h2d(out_ptr, np.full(min(out_cap, len(serial) + 256), 0xA5, np.uint8))
+            plan.execute()  # execute 2, beside execute 1's assembly; its own assembly rewrites the buffer
+            torch.cuda.synchronize()
+            fused = np.empty(len(serial), np.uint8)
+            ctx.d2h(fused, out_ptr)
+            plan.sync()
+            infos_p, piped = plan.download()
+        finally:
+            plan.close()
+    finally:
+        ctx.free(dev)
+    assert fused.tobytes() == serial
+    assert _table(infos_p) == _table(infos_s)
+    assert piped == serial
+    exp = oracle_encode_tiles(r, [wins[0], wins[-1]], level=level)
+    for k, i in enumerate((0, len(wins) - 1)):
+        s = infos_p[i]
+        assert piped[s.offset:s.offset + s.frame_bytes] == bytes(exp[k].body)
