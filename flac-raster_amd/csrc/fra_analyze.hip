@@ -555,6 +555,37 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 // enables was slower on 16-bit plans and the cap costs the analysis ~1 %
 #define FRA_ANA_SGPR 0
 #endif
+#ifndef FRA_PREFETCH
+// 16-bit full frames: one wave touches, during the Levinson-Durbin phase, the raw rows of the subframe
+// FRA_PREFETCH workgroups ahead in dispatch order (a multiple of 8: the same XCD, blocks being dealt
+// round-robin over the XCDs; 1536 = 6 workgroups per CU x 256 CUs, one residency generation), one dword
+// per 128-byte line, so that workgroup's load phase finds its rows in L2 / the Infinity Cache instead of
+// HBM: C4 k_analyze -2.2 %, C3 -2.3 % (r03 v11).  The 32-bit path does not take it (C5 +1.3 %: 16 KiB
+// of float rows per workgroup, r03 v12).  A hint only: nothing depends on it but the speed.  0 = off.
+#define FRA_PREFETCH 1536
+#endif
+template <typename T, int DIST>
+__device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {
+  const uint32_t nx = gridDim.x;
+  const uint64_t L = (uint64_t)blockIdx.x + (uint64_t)blockIdx.y * nx + DIST;
+  if (L >= (uint64_t)nx * gridDim.y) return 0u;
+  const int xp = (int)(L % nx), yp = (int)(L / nx);  // uniform
+  const FrameDev f2 = a.frames[a.frame_base + xp];
+  const StreamDev s2 = a.streams[f2.stream];
+  if (yp >= s2.channels || s2.ms || f2.n != kMaxBlock || s2.col_stride != 1) return 0u;
+  const char* b0 = (const char*)((const T*)a.raster + s2.base_off + (int64_t)yp * s2.band_stride +
+                                 (int64_t)f2.row0 * s2.row_stride);
+  const uint32_t w = (uint32_t)s2.width, rsb = (uint32_t)s2.row_stride * (uint32_t)sizeof(T);
+  // the 64-sample run of this lane (inside the subframe: n == 4096) spans <= 128 bytes: its first and
+  // last samples cover every line it touches (dword-aligned down)
+  auto word = [&](uint32_t c) -> uint32_t {
+    const uint32_t q = c / w;
+    return *(const uint32_t*)(b0 + ((q * rsb + (c - q * w) * (uint32_t)sizeof(T)) & ~3u));
+  };
+  const uint32_t c0 = (uint32_t)f2.col0 + 64u * (uint32_t)lane;
+  return word(c0) ^ word(c0 + 63u);
+}
+
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16))
 __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
@@ -592,6 +623,8 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
 #endif
 
   // ---- 1. load + normalise
+  uint32_t pf = 0u;  // prefetch words (FRA_PREFETCH), consumed at the end of the fast path
+  bool pf_ok = false;
   if (t < kSmpStride) S.smp[t] = 0;  // zero chunk (samples before the block start)
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
@@ -601,8 +634,10 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
     FRA_LOAD_STAMP(11, (int)np.mn + st.width + fr.n)
     bool done = false;
     if constexpr (!B32) {
-      if (FRA_FASTLOAD && lut && a.vec8 && a.off32 && n == kMaxBlock)
+      if (FRA_FASTLOAD && lut && a.vec8 && a.off32 && n == kMaxBlock) {
         done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
+        pf_ok = done;
+      }
     }
 #ifndef FRA_ONLYFAST
     if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
@@ -797,6 +832,11 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       // two FIXED candidates are searched meanwhile on the next two waves (psum is complete since the
       // autocorrelation barrier)
       const int nldw = (a.nwin + 3) >> 2;
+      if constexpr (!B32) {  // (levels 3-6: wave 3 idles during this phase)
+        if (FRA_PREFETCH > 0 && pf_ok && rw == 3)
+          pf = (src == ST_U16 || src == ST_I16) ? prefetch_rows<uint16_t, FRA_PREFETCH>(a, lane)
+                                                : prefetch_rows<uint8_t, FRA_PREFETCH>(a, lane);
+      }
       if (early && (rw == nldw || rw == nldw + 1)) {
         int g1, g2;
         fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
@@ -1157,6 +1197,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       const uint32_t nw = (fbits + 31) >> 5;
       if (verbatim) {  // straight from smp to the slot (the aliased bit buffer is not touched)
         verbatim_to_slot(a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride, S.smp, n, hdr, w, sbps, nw, t);
+        asm volatile("" ::"v"(pf));  // (the prefetch loads stay; they returned long ago)
         return;
       }
       // the bit buffer aliases smp, dead since the barrier above (warm-up samples in S.warm)
@@ -1214,6 +1255,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       {
         uint32_t* slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
         for (uint32_t j = t; j < nw; j += kThreads) slot[j] = buf[j];
+        asm volatile("" ::"v"(pf));
         FRA_STAMP(10)
         return;
       }

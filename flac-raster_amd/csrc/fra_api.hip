@@ -641,10 +641,10 @@ static int plan_build(fra_plan* p) {
   for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
   {  // second buffer set for cross-execute pipelining
     const char* ev = getenv("FRA_PIPE");
-    // large plans only: small ones (the pyflac shim, single tiles) execute once per plan, and the
-    // measured gain is the tail of k_analyze (k_assemble cannot co-reside with it: 6 analysis workgroups
-    // leave 32 VGPRs and 7.9 KiB of LDS per CU/SIMD) -- C3 1.610 -> 1.586 ms, C4 2.422 -> 2.408 ms
-    const bool want = !(ev && atoi(ev) == 0) && p->groups.size() == 1 && nfr >= 4096;
+    // large plans only (>= 1024 frames: a C4 scene split 8 ways, ~3.7k frames per rank, stays
+    // pipelined); small ones (the pyflac shim, single tiles) execute once per plan
+    static const int min_frames = getenv("FRA_PIPE_MIN_FRAMES") ? atoi(getenv("FRA_PIPE_MIN_FRAMES")) : 1024;
+    const bool want = !(ev && atoi(ev) == 0) && p->groups.size() == 1 && nfr >= min_frames;
     const size_t nsf = (size_t)nfr * p->cmax;
     const size_t nst = std::max<size_t>(1, p->streams.size());
     const size_t extra = sizeof(SfDesc) * nsf + sizeof(uint32_t) * (size_t)p->tmp_stride * nsf +

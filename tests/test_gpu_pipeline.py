@@ -203,7 +203,11 @@ def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level,
     execute 2, written into an output buffer poisoned after execute 1 and read after a device-wide barrier,
     must be byte-identical to the serial (timing-mode) execute's; so must the plan's own download; and
     sampled tiles must equal the oracle's frames."""
-    import torch  # device-wide barrier (hipDeviceSynchronize) independent of the plan's own sync
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")  # the HIP runtime the product library runs on (one per process)
+
+    def device_barrier():  # hipDeviceSynchronize: every stream of the device, independent of the plan's sync
+        assert hip.hipDeviceSynchronize() == 0
 
     r = synth_window(kind, 91, bands, H, W).astype(dtype, copy=False)
     wins = calculate_tiles(H, W, tile)
@@ -221,10 +225,10 @@ def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level,
             infos_s, serial = plan.download()
             plan.enable_timing(False)
             plan.execute()  # execute 1
-            torch.cuda.synchronize()
+            device_barrier()
             ctx.h2d(out_ptr, np.full(min(out_cap, len(serial) + 256), 0xA5, np.uint8))
             plan.execute()  # execute 2, beside execute 1's assembly; its own assembly rewrites the buffer
-            torch.cuda.synchronize()
+            device_barrier()
             fused = np.empty(len(serial), np.uint8)
             ctx.d2h(fused, out_ptr)
             plan.sync()
