@@ -133,6 +133,10 @@ struct fra_plan {
   unsigned long long* fbytes2[2] = {};
   unsigned long long* foff2[2] = {};
   hipStream_t pack = nullptr;
+  // the analysis of buffer set b runs on astream[b] (highest priority): execute k+1's k_analyze is queued
+  // on the other stream than execute k's, so its first workgroups fill the CUs that execute k's tail
+  // leaves idle instead of waiting for that kernel to end (16-bit plans; FRA_DUAL_ANA=0/1 forces)
+  hipStream_t astream[2] = {};
   hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
   bool pack_pending[2] = {false, false};
   // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
@@ -313,6 +317,8 @@ void fra_plan_destroy(fra_plan* p) {
   }
   if (p->pack) (void)hipStreamDestroy(p->pack);
   if (p->nstream) (void)hipStreamDestroy(p->nstream);
+  for (auto& st : p->astream)
+    if (st) (void)hipStreamDestroy(st);
   for (int b = 0; b < 2; b++) {
     if (p->ev_scan[b]) (void)hipEventDestroy(p->ev_scan[b]);
     if (p->ev_pack[b]) (void)hipEventDestroy(p->ev_pack[b]);
@@ -674,6 +680,12 @@ static int plan_build(fra_plan* p) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(hipStreamCreateWithPriority(&p->pack, hipStreamNonBlocking, lo));
+        // 16-bit plans: C4 -1.2 %, C3 -2.4 %; 32-bps plans keep one analysis stream (C5 +5 %: the early
+        // start takes the slots the background assembly was using) (r03 v14)
+        static const int dual_env = getenv("FRA_DUAL_ANA") ? atoi(getenv("FRA_DUAL_ANA")) : -1;
+        const bool dual = dual_env < 0 ? !p->b32 : dual_env != 0;
+        if (dual)
+          for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
       }
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
@@ -713,6 +725,9 @@ static int drain_pipeline(fra_plan* p) {
       HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_pack[b], 0));
       p->pack_pending[b] = false;
     }
+    // (an analysis on astream[b] is followed by its chain + assembly on the pack stream: covered above;
+    // the wait below also orders a pipelined execute's analysis before the serial work that follows)
+    if (p->ana_pending[b] && p->astream[b]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
     p->ana_pending[b] = false;  // (covered by the resync below)
   }
   // serial executes and host raster copies now go onto the plan's stream; when pipelining resumes, the
@@ -725,6 +740,8 @@ static int drain_pipeline(fra_plan* p) {
   return FRA_OK;
 }
 static int plan_sync_all(fra_plan* p) {
+  for (auto& st : p->astream)
+    if (st) HIPCHK(hipStreamSynchronize(st));
   if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
   if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));
@@ -738,6 +755,9 @@ int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
     p->d_raster = raster;
   } else {
     if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
+    // the copy must not overtake a pipelined analysis (its own stream) still reading the old rows
+    for (int b = 0; b < 2; b++)
+      if (p->ana_pending[b] && p->astream[b]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
     if (p->raster_bytes) {
       HIPCHK(hipMemcpyAsync(p->d_raster_owned, raster, p->raster_bytes, hipMemcpyHostToDevice, p->ctx->stream));
       if (p->pipe) {  // the next pipelined norm stage (norm stream) reads the new raster after this copy
@@ -882,7 +902,8 @@ int fra_plan_execute(fra_plan* p) {
   if (p->pipe && !p->timing) {
     // cross-execute pipelining: this execute's analysis overlaps the previous execute's k_assemble
     const int b = p->cur ^ 1;
-    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(s, p->ev_pack[b], 0));  // execute k-2 is done with set b
+    const hipStream_t as = p->astream[b] ? p->astream[b] : s;  // this execute's analysis stream
+    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(as, p->ev_pack[b], 0));  // execute k-2 is done with set b
     // one background kernel at a time beside k_analyze: this norm stage after k_assemble of execute k-2
     // (which runs under the analysis of execute k-1)
     if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_pack[b], 0));
@@ -892,6 +913,8 @@ int fra_plan_execute(fra_plan* p) {
     if (p->ana_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_ana[b], 0));
     if (p->resync) {  // first pipelined execute after serial ones: after everything on the plan's stream
       HIPCHK(hipEventRecord(p->ev_raster, s));
+      for (auto& st : p->astream)
+        if (st) HIPCHK(hipStreamWaitEvent(st, p->ev_raster, 0));
       p->raster_dirty = true;
       p->resync = false;
     }
@@ -899,7 +922,7 @@ int fra_plan_execute(fra_plan* p) {
       HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_raster, 0));
       p->raster_dirty = false;
     }
-    rc = run_group(p, p->groups[0], 0, 1, s, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
+    rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
                    p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
     if (rc) return rc;
     p->ana_pending[b] = true;
