@@ -326,11 +326,13 @@ __device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDe
       }
     }
   }
+  FRA_LOAD_STAMP(12, (int)x[0].v[0] + (int)x[NV - 1].v[V - 1])
   int32_t g[NV * V];
 #pragma unroll
   for (int kv = 0; kv < NV; kv++)
 #pragma unroll
     for (int e = 0; e < V; e++) g[kv * V + e] = lut[lut_index<SRC>(x[kv].v[e])];
+  FRA_LOAD_STAMP(13, g[0] + g[NV * V - 1])
   uint32_t orp = 0;
   i16x2 pmin = {32767, 32767}, pmax = {-32768, -32768};
 #pragma unroll
