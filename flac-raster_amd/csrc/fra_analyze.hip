@@ -31,8 +31,16 @@ namespace fra { extern __device__ unsigned long long g_fra_stamps[]; }
 #define FRA_LOAD_STAMP(k, dep)                                                                       \
   if (threadIdx.x == 0 && (dep) != 0x7FFFFFF1) {                                                     \
     const unsigned wgi_ = blockIdx.x * gridDim.y + blockIdx.y;                                       \
-    if (wgi_ < (1u << 17)) g_fra_stamps[wgi_ * 16u + (k)] = __builtin_amdgcn_s_memtime();            \
+    if (wgi_ < (1u << 17)) g_fra_stamps[wgi_ * 20u + (k)] = __builtin_amdgcn_s_memtime();            \
   }
+// lane 0 of the calling wave (per-role finish times inside a phase)
+#define FRA_ROLE_STAMP(k)                                                                            \
+  if ((threadIdx.x & 63) == 0) {                                                                     \
+    const unsigned wgi_ = blockIdx.x * gridDim.y + blockIdx.y;                                       \
+    if (wgi_ < (1u << 17)) g_fra_stamps[wgi_ * 20u + (k)] = __builtin_amdgcn_s_memtime();            \
+  }
+#else
+#define FRA_ROLE_STAMP(k)
 #endif
 #include "fra_device.h"
 
@@ -42,7 +50,7 @@ namespace fra {
 // diagnostic build only (csrc/Makefile `stamps`, tools/stamp_phases.py): wave 0 of the first kStampWG
 // workgroups stores s_memtime after each phase barrier, so phase durations are measured inside the
 // real, mixed steady state (every other workgroup keeps running the full kernel)
-constexpr unsigned kStampWG = 1u << 17, kStampN = 16;
+constexpr unsigned kStampWG = 1u << 17, kStampN = 20;
 __device__ unsigned long long g_fra_stamps[kStampWG * kStampN];
 #define FRA_STAMP(k)                                                                          \
   if (threadIdx.x == 0) {                                                                      \
@@ -852,6 +860,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
             S.mporder[m] = bp;
           }
         }
+        if (rw == nldw) { FRA_ROLE_STAMP(16) } else { FRA_ROLE_STAMP(17) }
       }
       if (rw < nldw) {
         const int gw = lane >> 4, lo = lane & 15;
@@ -901,6 +910,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
 #pragma unroll
           for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
         }
+        FRA_ROLE_STAMP(15)
       }
     }
   }
@@ -1017,6 +1027,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
     }
+    FRA_ROLE_STAMP(18)
   }
   {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share
     static_assert(kMaxPart * 3 <= 2 * (2 * kMaxPart), "esum2 inside node[0..1]");

@@ -26,7 +26,7 @@ cfgname = args[0] if args else "c4"
 cfg = dict(bench.CONFIGS[cfgname])
 if len(args) > 1:
     cfg["level"] = int(args[1])
-KWG, KN = 1 << 17, 16
+KWG, KN = 1 << 17, 20
 NAMES = ["load+normalise+reduce", "FIXED sums", "autocorrelation", "LD/quantise + FIXED search",
          "LPC residual sums", "partition search", "winner residuals + Rice sums", "exact bits + scan",
          "encode", "slot write"]
@@ -73,6 +73,15 @@ if FINE:
     for nm, a, b in sub:
         x = f[:, b] - f[:, a]
         print(f"  {nm:34s} {np.median(x):9.0f} {x.mean():9.0f}")
+if FINE:  # per-role finish times inside the Levinson-Durbin phase (from its start, stamp 3) and the search
+    f = st[fast]
+    for nm, k, a in (("LD/quantise wave done", 15, 3), ("FIXED search wave 1 done", 16, 3),
+                     ("FIXED search wave 2 done", 17, 3), ("LD phase barrier passed", 4, 3),
+                     ("LPC search wave done", 18, 5), ("search barrier passed", 6, 5)):
+        ok = (f[:, k] > 0) & (f[:, a] > 0)
+        if ok.any():
+            x = f[ok, k] - f[ok, a]
+            print(f"  {nm:34s} {np.median(x):9.0f} {x.mean():9.0f}  ({int(ok.sum())} workgroups)")
 span = st[fast, 10].max() - st[fast, 0].min()
 print(f"launch span of stamped workgroups: {span} cycles; mean concurrent workgroups {tot.sum() / span:.1f}")
 plan.close()
