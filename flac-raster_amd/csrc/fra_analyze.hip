@@ -563,6 +563,9 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 // enables was slower on 16-bit plans and the cap costs the analysis ~1 %
 #define FRA_ANA_SGPR 0
 #endif
+#ifndef FRA_PRIO
+#define FRA_PRIO 0  // s_setprio level of the single-wave phases (0 = off)
+#endif
 #ifndef FRA_PREFETCH
 // 16-bit full frames: one wave touches, during the Levinson-Durbin phase, the raw rows of the subframe
 // FRA_PREFETCH workgroups ahead in dispatch order (a multiple of 8: the same XCD, blocks being dealt
@@ -863,6 +866,9 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
         if (rw == nldw) { FRA_ROLE_STAMP(16) } else { FRA_ROLE_STAMP(17) }
       }
       if (rw < nldw) {
+        // the Levinson-Durbin wave is the pole of this phase (r03 v18 stamps): FRA_PRIO raises its issue
+        // priority over the other waves of its SIMD for the recursion
+        if (FRA_PRIO) __builtin_amdgcn_s_setprio(FRA_PRIO);
         const int gw = lane >> 4, lo = lane & 15;
         const int wi = 4 * rw + gw;
         const bool gon = wi < a.nwin;
@@ -910,6 +916,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
 #pragma unroll
           for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
         }
+        if (FRA_PRIO) __builtin_amdgcn_s_setprio(0);
         FRA_ROLE_STAMP(15)
       }
     }
@@ -1018,6 +1025,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
   }
   for (int m = (early ? 5 : 0) + rw; m < nmod; m += 4) {
     if (!S.mvalid[m] || (m < 5 && m != fg1 && m != fg2)) continue;
+    if (FRA_PRIO) __builtin_amdgcn_s_setprio(FRA_PRIO);  // (single-wave pole, as the LD above)
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
@@ -1027,6 +1035,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
     }
+    if (FRA_PRIO) __builtin_amdgcn_s_setprio(0);
     FRA_ROLE_STAMP(18)
   }
   {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share

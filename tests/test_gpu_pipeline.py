@@ -244,3 +244,42 @@ def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level,
     for k, i in enumerate((0, len(wins) - 1)):
         s = infos_p[i]
         assert piped[s.offset:s.offset + s.frame_bytes] == bytes(exp[k].body)
+
+
+def test_host_raster_swap_between_pipelined_executes():
+    """A host raster set between pipelined executes (no sync) is copied into the plan's device buffer on the
+    plan's stream; with each buffer set's analysis on its own stream, the copy must wait for the analyses
+    still reading the old rows.  Outputs after the swap equal a fresh plan's on the new raster, and the
+    executes before it a fresh plan's on the old one."""
+    H, W = 4096, 4096
+    a = synth_window(4, 5, 1, H, W).astype(np.uint16)
+    b = synth_window(4, 6, 1, H, W).astype(np.uint16)
+    wins = calculate_tiles(H, W, 1024)
+    ctx = N.default_context(0)
+
+    def fresh(r):
+        p = N.Plan(ctx, r.ctypes.data, False, r.dtype, 1, (H * W, W, 1), wins, 5, 4096, 16, keepalive=r)
+        try:
+            p.execute()
+            return p.download()[1]
+        finally:
+            p.close()
+
+    exp_a, exp_b = fresh(a), fresh(b)
+    assert exp_a != exp_b
+    plan = N.Plan(ctx, a.ctypes.data, False, a.dtype, 1, (H * W, W, 1), wins, 5, 4096, 16, keepalive=a)
+    try:
+        assert plan.flags() & 2
+        plan.execute()
+        plan.execute()
+        plan.sync()
+        assert plan.download()[1] == exp_a
+        plan.execute()
+        plan.execute()  # two analyses in flight (one per buffer set) when the copy of b is queued
+        plan.set_raster(b.ctypes.data, False, keepalive=b)
+        plan.execute()
+        plan.execute()
+        plan.sync()
+        assert plan.download()[1] == exp_b
+    finally:
+        plan.close()
