@@ -569,11 +569,12 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
 #ifndef FRA_PREFETCH
 // 16-bit full frames: one wave touches, during the Levinson-Durbin phase, the raw rows of the subframe
 // FRA_PREFETCH workgroups ahead in dispatch order (a multiple of 8: the same XCD, blocks being dealt
-// round-robin over the XCDs; 1536 = 6 workgroups per CU x 256 CUs, one residency generation), one dword
-// per 128-byte line, so that workgroup's load phase finds its rows in L2 / the Infinity Cache instead of
-// HBM: C4 k_analyze -2.2 %, C3 -2.3 % (r03 v11).  The 32-bit path does not take it (C5 +1.3 %: 16 KiB
-// of float rows per workgroup, r03 v12).  A hint only: nothing depends on it but the speed.  0 = off.
-#define FRA_PREFETCH 1536
+// round-robin over the XCDs; 1024-1536 ~ the workgroups resident at 6 per CU x 256 CUs), one dword per
+// 128-byte line, so that workgroup's load phase finds its rows in L2 / the Infinity Cache instead of HBM:
+// C4 k_analyze -2.2 %, C3 -2.3 % at 1536 (r03 v11); 1024 another -0.5 % on the step, 768 / 2048 / 3072
+// no better (r03 v11, v19).  The 32-bit path does not take it (C5 +1.3 %: 16 KiB of float rows per
+// workgroup, r03 v12).  A hint only: nothing depends on it but the speed.  0 = off.
+#define FRA_PREFETCH 1024
 #endif
 template <typename T, int DIST>
 __device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {

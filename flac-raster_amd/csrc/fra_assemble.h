@@ -61,18 +61,18 @@ __device__ __forceinline__ uint32_t gf16_mul_dev(uint32_t a, uint32_t b) {
 struct alignas(16) AssembleSmem {
   uint16_t T[16][256];  // slice-by-16: T[k][v] = CRC of v followed by k zero bytes
   uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..12 (tree 4..9, waves 10..11, Horner 12)
-  uint32_t meta[kMetaWords];  // this frame's header words and blob bit bounds (k_frame_bytes)
+  uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_bytes); [wave]
   uint32_t crcw[4];
-  uint32_t tailw;       // the output window of the last, partial dword (bytes [4*NF - A, L))
+  uint32_t tailw[4];    // the output window of the last, partial dword (bytes [4*NF - A, L)); [wave]
 };
 // background form: only the per-quad tables in LDS (9.3 KiB: it fits beside four 32-bps k_analyze
 // workgroups too); the once-per-frame tree levels 4..11 are read from global memory (L1/L2 resident)
 struct alignas(16) AssembleSmemBg {
   uint16_t T[16][256];
   uint16_t M12[512];    // multiply by x^(8*2^12) (the Horner step)
-  uint32_t meta[kMetaWords];
+  uint32_t meta[1][kMetaWords];
   uint32_t crcw[4];
-  uint32_t tailw;
+  uint32_t tailw[1];
 };
 
 // `take` (1..32) bits at bit b of a big-endian word array, right-aligned
@@ -102,21 +102,28 @@ __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
   }
 }
 
-// one frame by the whole workgroup, U quads per thread per round.  Header and blob bounds come
-// precomputed from k_frame_bytes, so every metadata load is issued in the first round; TABLES: the CRC
-// tables are copied here, while the first slot loads are in flight (one workgroup per frame)
-template <int U, bool TABLES, typename SM>
+// one frame by NT threads -- the whole workgroup (NT = 256) or one wave (NT = 64: four frames per
+// workgroup, no workgroup barrier per frame, the CRC tables copied once for the four) -- U quads per
+// thread per round.  Header and blob bounds come precomputed from k_frame_bytes, so every metadata load is
+// issued in the first round; TABLES (NT = 256): the CRC tables are copied here, while the first slot loads
+// are in flight (one workgroup per frame)
+template <int U, bool TABLES, typename SM, int NT = kThreads>
 __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM& S) {
-  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  static_assert(NT == kThreads || NT == 64, "a frame per workgroup or per wave");
+  const int lane = (int)threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int t = NT == 64 ? lane : (int)threadIdx.x;  // thread index within the frame's group
   constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
+  static_assert(!kBg || NT == kThreads, "background form: one frame per workgroup");
+  uint32_t* const meta = S.meta[NT == 64 ? wv : 0];
+  uint32_t& tailw = S.tailw[NT == 64 ? wv : 0];
   const uint16_t* M;     // tree / wave levels kMLo..11
-  const uint16_t* Mh;    // the Horner level 12
+  const uint16_t* Mh;    // the Horner level: x^(128 NT) = x^(8 * 2^12) (NT = 256) or x^(8 * 2^10) (NT = 64)
   if constexpr (kBg) {
     M = a.crctab + 1024 + kMLo * 512;
     Mh = &S.M12[0];
   } else {
     M = &S.M[0][0];
-    Mh = &S.M[12 - kMLo][0];
+    Mh = &S.M[(NT == 64 ? 10 : 12) - kMLo][0];
   }
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
@@ -129,8 +136,8 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   uint32_t sg[kMaxChannels + 2];  // wave-uniform blob boundaries (bits)
 #pragma unroll
   for (int i = 0; i < kMaxChannels + 2; i++) sg[i] = __builtin_amdgcn_readfirstlane(gmeta[kHdrWords + i]);
-  const uint32_t* hdrw = S.meta;
-  const uint32_t* seg = S.meta + kHdrWords;
+  const uint32_t* hdrw = meta;
+  const uint32_t* seg = meta + kHdrWords;
   uint32_t TB = sg[1];                          // frame bits before the byte pad: sg[C + 1]
 #pragma unroll
   for (int i = 2; i < kMaxChannels + 2; i++) TB = (i == C + 1) ? sg[i] : TB;  // (no dynamic index: no scratch)
@@ -141,7 +148,7 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   const int a4 = (int)(((F - A) >> 2) & 3);
   const int NQ = (NF + a4 + 3) >> 2;       // quads holding CRC dwords
   const int NQW = (ND + a4 + 3) >> 2;      // quads holding output dwords (NQ or NQ + 1)
-  const int pad = (int)((kThreads - (NQ % kThreads)) % kThreads);
+  const int pad = (int)((NT - (NQ % NT)) % NT);
   const int kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
   // slot of output channels 0 / 1 (k_frame_bytes: identity unless a mid-side assignment was chosen)
@@ -188,19 +195,19 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
 
   uint32_t acc = 0;
   int q0 = (int)t - pad;  // quad index in v/4 space
-  if (q0 < 0) q0 += kThreads;
+  if (q0 < 0) q0 += NT;
   // slot gather of the U quads of round q0 (fast case: one 16-byte + one dword load, shift later)
   // sh[u] = the funnel shift of a fast quad, kSlow (no single-blob window: the dword-wise path)
   constexpr uint32_t kSlow = 0xFFFFFFFFu;
   auto fetch = [&](const int qr, uint32_t (&w)[U][5], uint32_t (&sh)[U]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int k = 4 * (qr + (int)u * kThreads) - a4;  // first dword of the quad
+      const int k = 4 * (qr + (int)u * NT) - a4;  // first dword of the quad
       const int bp = 8 * (4 * k - (int)A);
       sh[u] = kSlow;
 #pragma unroll
       for (int i = 0; i < 5; i++) w[u][i] = 0;
-      if (qr + (int)u * kThreads < NQW && k >= 0 && k + 4 <= ND && bp >= (int)sg[1] && bp + 128 <= (int)TB) {
+      if (qr + (int)u * NT < NQW && k >= 0 && k + 4 <= ND && bp >= (int)sg[1] && bp + 128 <= (int)TB) {
         const uint32_t b = (uint32_t)bp;
         // blob sgi - 1 holds bit b: lo = sg[sgi] <= b < hi = sg[sgi + 1] (b < TB: never past blob C - 1);
         // a select chain, not a dynamically indexed array (which would live in scratch)
@@ -235,9 +242,15 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   if (q0 < NQW) fetch(q0, wn, shn);
   // CRC tables and header words to LDS while the first slot loads are in flight
   if constexpr (TABLES) copy_tables(a, S);
-  if (t < kMetaWords) S.meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
-  __syncthreads();
-  for (; q0 < NQW; q0 += (int)kThreads * U) {
+  if (t < kMetaWords) meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
+  if constexpr (NT == 64) {  // this wave's LDS stores -> its own reads
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+  for (; q0 < NQW; q0 += NT * U) {
     uint32_t w[U][5], sh[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -246,10 +259,10 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
       for (int i = 0; i < 5; i++) w[u][i] = wn[u][i];
     }
     // next round's loads are in flight while this round is shifted, stored and CRC'd
-    if (q0 + (int)kThreads * U < NQW) fetch(q0 + (int)kThreads * U, wn, shn);
+    if (q0 + NT * U < NQW) fetch(q0 + NT * U, wn, shn);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int q = q0 + (int)u * kThreads;
+      const int q = q0 + (int)u * NT;
       if (q >= NQW) break;
       const int k = 4 * q - a4;
       uint32_t val[4];
@@ -287,7 +300,7 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
               if (fb >= 0 && fb < (int)L) a.out[F + fb] = (uint8_t)(val[i] >> (24 - 8 * b));
             }
           }
-          if (kk == NF) S.tailw = val[i];
+          if (kk == NF) tailw = val[i];
           if (kk >= NF) val[i] = 0;  // trailing zeros in the CRC (removed below)
         }
       }
@@ -298,7 +311,7 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
           c ^= (uint32_t)S.T[15 - 4 * i][val[i] >> 24] ^ (uint32_t)S.T[14 - 4 * i][(val[i] >> 16) & 0xFF] ^
                (uint32_t)S.T[13 - 4 * i][(val[i] >> 8) & 0xFF] ^ (uint32_t)S.T[12 - 4 * i][val[i] & 0xFF];
         }
-        acc = crc_mul_tab(Mh, acc) ^ c;  // Horner step: x^(128*256)
+        acc = crc_mul_tab(Mh, acc) ^ c;  // Horner step: x^(128 NT)
       }
     }
   }
@@ -309,12 +322,25 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   acc ^= crc_mul(M, 7, dpp32<DPP_SHR8, 0xF>(acc));
   acc ^= crc_mul(M, 8, dpp32<DPP_BC15, 0xA>(acc));
   acc ^= crc_mul(M, 9, dpp32<DPP_BC31, 0xC>(acc));
-  if (lane == 63) S.crcw[wv] = acc;
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t c01 = crc_mul(M, 10, S.crcw[0]) ^ S.crcw[1];
-    const uint32_t c23 = crc_mul(M, 10, S.crcw[2]) ^ S.crcw[3];
-    uint32_t crc = crc_mul(M, 11, c01) ^ c23;
+  bool last;  // the thread that finishes the frame
+  uint32_t crc;
+  if constexpr (NT == 64) {  // the wave's accumulators are the frame's: lane 63 holds the CRC
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // tailw (any lane) -> lane 63
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    last = lane == 63;
+    crc = acc;
+  } else {
+    if (lane == 63) S.crcw[wv] = acc;
+    __syncthreads();
+    last = t == 0;
+    if (last) {
+      const uint32_t c01 = crc_mul(M, 10, S.crcw[0]) ^ S.crcw[1];
+      const uint32_t c23 = crc_mul(M, 10, S.crcw[2]) ^ S.crcw[3];
+      crc = crc_mul(M, 11, c01) ^ c23;
+    }
+  }
+  if (last) {
     // remove the e zero dwords that followed dword NF-1 inside the last CRC quad: * x^(-32e)
     const int e = (int)(4 * NQ - (NF + a4));
     constexpr uint32_t kInvX32[4] = {0x0001u, 0xCAA8u, 0x25DDu, 0x37B1u};  // x^(-32e) mod P
@@ -322,7 +348,7 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
     // tail: frame bytes [4*NF - A, L) not covered by whole dwords
     const int tb0 = 4 * NF - (int)A;
     if (tb0 < (int)L) {
-      const uint32_t val = S.tailw;
+      const uint32_t val = tailw;
       for (int fb = tb0; fb < (int)L; fb++) {
         const uint32_t by = (val >> (24 - 8 * (int)(fb - tb0))) & 0xFF;
         crc = ((crc << 8) ^ S.T[0][((crc >> 8) ^ by) & 0xFF]) & 0xFFFF;

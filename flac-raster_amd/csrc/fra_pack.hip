@@ -3,6 +3,8 @@
 // * k_assemble: serial executes and the host pipeline, one workgroup per frame;
 // * k_assemble_bg: background form (see below);
 // * the pipelined execute fuses the assembly of execute k into the tail of execute k+1's k_analyze.
+#include <cstdlib>
+
 #include "fra_assemble.h"
 
 namespace fra {
@@ -30,10 +32,27 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), 
   }
 }
 
+// four frames per workgroup, one per wave (FRA_ASM_WAVE=1): the CRC tables are copied to LDS once for
+// the four and a frame needs no workgroup barrier
+template <int U>
+__global__ void __launch_bounds__(kThreads, U > 2 ? 6 : 8) k_assemble4(JobArgs a) {
+  __shared__ AssembleSmem S;
+  copy_tables(a, S);
+  __syncthreads();
+  const int i = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  if (i < a.frame_count) assemble_frame<U, false, AssembleSmem, 64>(a, a.frame_base + i, S);
+}
+
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks) {
   if (a.frame_count <= 0) return hipSuccess;
   if (bg_blocks > 0) k_assemble_bg<<<(unsigned)std::min(bg_blocks, a.frame_count), kThreads, 0, s>>>(a);
-  else k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);
+  else {
+    static const int wave = getenv("FRA_ASM_WAVE") ? atoi(getenv("FRA_ASM_WAVE")) : 0;
+    const unsigned g4 = (unsigned)((a.frame_count + 3) / 4);
+    if (wave == 1) k_assemble4<2><<<g4, kThreads, 0, s>>>(a);
+    else if (wave == 2) k_assemble4<4><<<g4, kThreads, 0, s>>>(a);
+    else k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);
+  }
   return hipGetLastError();
 }
 
