@@ -69,10 +69,10 @@ struct alignas(16) AssembleSmem {
 // workgroups too); the once-per-frame tree levels 4..11 are read from global memory (L1/L2 resident)
 struct alignas(16) AssembleSmemBg {
   uint16_t T[16][256];
-  uint16_t M12[512];    // multiply by x^(8*2^12) (the Horner step)
-  uint32_t meta[1][kMetaWords];
+  uint16_t Mh[512];     // the Horner step: x^(8*2^12) (a frame per workgroup) or x^(8*2^10) (per wave)
+  uint32_t meta[4][kMetaWords];
   uint32_t crcw[4];
-  uint32_t tailw[1];
+  uint32_t tailw[4];
 };
 
 // `take` (1..32) bits at bit b of a big-endian word array, right-aligned
@@ -86,19 +86,19 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 }
 
 // CRC tables to LDS (16-byte loads) so no step of the CRC chain waits on a global gather
-template <typename SM>
+template <typename SM, int NT = kThreads>
 __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
   constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
   const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
-  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kBg ? 12 : kMLo) * 512);
+  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kBg ? (NT == 64 ? 10 : 12) : kMLo) * 512);
   uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
   uint4* dM;
-  if constexpr (kBg) dM = reinterpret_cast<uint4*>(&S.M12[0]);
+  if constexpr (kBg) dM = reinterpret_cast<uint4*>(&S.Mh[0]);
   else dM = reinterpret_cast<uint4*>(&S.M[0][0]);
-  constexpr int NT = 16 * 256 * 2 / 16, NM = (kBg ? 1 : kMLevels) * 512 * 2 / 16;
-  for (int i = (int)threadIdx.x; i < NT + NM; i += kThreads) {
-    if (i < NT) dT[i] = srcT[i];
-    else dM[i - NT] = srcM[i - NT];
+  constexpr int NTV = 16 * 256 * 2 / 16, NMV = (kBg ? 1 : kMLevels) * 512 * 2 / 16;  // uint4 counts
+  for (int i = (int)threadIdx.x; i < NTV + NMV; i += kThreads) {
+    if (i < NTV) dT[i] = srcT[i];
+    else dM[i - NTV] = srcM[i - NTV];
   }
 }
 
@@ -113,14 +113,13 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   const int lane = (int)threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int t = NT == 64 ? lane : (int)threadIdx.x;  // thread index within the frame's group
   constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
-  static_assert(!kBg || NT == kThreads, "background form: one frame per workgroup");
   uint32_t* const meta = S.meta[NT == 64 ? wv : 0];
   uint32_t& tailw = S.tailw[NT == 64 ? wv : 0];
   const uint16_t* M;     // tree / wave levels kMLo..11
   const uint16_t* Mh;    // the Horner level: x^(128 NT) = x^(8 * 2^12) (NT = 256) or x^(8 * 2^10) (NT = 64)
-  if constexpr (kBg) {
+  if constexpr (kBg) {  // (copy_tables<SM, NT> put the matching Horner level in S.Mh)
     M = a.crctab + 1024 + kMLo * 512;
-    Mh = &S.M12[0];
+    Mh = &S.Mh[0];
   } else {
     M = &S.M[0][0];
     Mh = &S.M[(NT == 64 ? 10 : 12) - kMLo][0];

@@ -1,15 +1,19 @@
 // fra_pack.hip -- the frame assembly kernels (one frame per workgroup; the per-frame device code, its
 // gather formulation and the CRC-16 scheme are in fra_assemble.h):
-// * k_assemble: serial executes and the host pipeline, one workgroup per frame;
+// * k_assemble4 (default: one frame per wave, four per workgroup) / k_assemble (one per workgroup);
 // * k_assemble_bg: background form (see below);
 // * the pipelined execute fuses the assembly of execute k into the tail of execute k+1's k_analyze.
 #include <cstdlib>
 
 #include "fra_assemble.h"
 
+#ifndef FRA_BG_PER_WAVE
+#define FRA_BG_PER_WAVE 1
+#endif
+
 namespace fra {
 
-// one workgroup per frame (serial executes: the kernel has the device to itself)
+// one workgroup per frame (FRA_ASM_WAVE=0; the r02 form)
 __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
   __shared__ AssembleSmem S;
   assemble_frame<2, true>(a, a.frame_base + (int)blockIdx.x, S);
@@ -25,33 +29,41 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
 __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_num_vgpr(16),
                                amdgpu_num_sgpr(96))) k_assemble_bg(JobArgs a) {
   __shared__ AssembleSmemBg S;
+#if FRA_BG_PER_WAVE
+  // one frame per wave, each wave striding over the frames on its own (no workgroup barrier per frame)
+  copy_tables<AssembleSmemBg, 64>(a, S);
+  __syncthreads();
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  for (int i = (int)blockIdx.x * 4 + w; i < a.frame_count; i += (int)gridDim.x * 4)
+    assemble_frame<1, false, AssembleSmemBg, 64>(a, a.frame_base + i, S);
+#else
   copy_tables(a, S);
   for (int i = (int)blockIdx.x; i < a.frame_count; i += (int)gridDim.x) {
     __syncthreads();  // the previous frame's readers of S.meta / S.crcw / S.tailw are done
     assemble_frame<1, false>(a, a.frame_base + i, S);
   }
+#endif
 }
 
-// four frames per workgroup, one per wave (FRA_ASM_WAVE=1): the CRC tables are copied to LDS once for
-// the four and a frame needs no workgroup barrier
-template <int U>
-__global__ void __launch_bounds__(kThreads, U > 2 ? 6 : 8) k_assemble4(JobArgs a) {
+// the default: four frames per workgroup, one per wave -- the 17.5 KiB of CRC tables are copied to LDS
+// once for four frames (a C3 frame is only ~7 KiB) and a frame needs no workgroup barrier.  r03 v20: C4
+// k_assemble 0.302 -> 0.272 ms (step 2.03 -> 1.98 ms), C3 0.310 -> 0.209 ms (step 1.38 -> 1.27 ms); two quads
+// per thread per round beat four (`profiles/r03_ab_assemble_per_wave_v20.txt`)
+__global__ void __launch_bounds__(kThreads, 8) k_assemble4(JobArgs a) {
   __shared__ AssembleSmem S;
   copy_tables(a, S);
   __syncthreads();
   const int i = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  if (i < a.frame_count) assemble_frame<U, false, AssembleSmem, 64>(a, a.frame_base + i, S);
+  if (i < a.frame_count) assemble_frame<2, false, AssembleSmem, 64>(a, a.frame_base + i, S);
 }
 
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks) {
   if (a.frame_count <= 0) return hipSuccess;
   if (bg_blocks > 0) k_assemble_bg<<<(unsigned)std::min(bg_blocks, a.frame_count), kThreads, 0, s>>>(a);
   else {
-    static const int wave = getenv("FRA_ASM_WAVE") ? atoi(getenv("FRA_ASM_WAVE")) : 0;
-    const unsigned g4 = (unsigned)((a.frame_count + 3) / 4);
-    if (wave == 1) k_assemble4<2><<<g4, kThreads, 0, s>>>(a);
-    else if (wave == 2) k_assemble4<4><<<g4, kThreads, 0, s>>>(a);
-    else k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);
+    static const bool per_wg = getenv("FRA_ASM_WAVE") && atoi(getenv("FRA_ASM_WAVE")) == 0;
+    if (per_wg) k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);  // one frame per workgroup
+    else k_assemble4<<<(unsigned)((a.frame_count + 3) / 4), kThreads, 0, s>>>(a);
   }
   return hipGetLastError();
 }
