@@ -1,9 +1,7 @@
 #!/bin/bash
 # Round-3 GPU call (rewritten per call; git history keeps each version).  Usage: bash tools/gpu_r03.sh <tag>
-# v26: the frame-size chain of small frame groups as ONE single-workgroup launch (k_frame_chain1, groups of
-# <= 4096 frames; FRA_CHAIN1=0 = the k_frame_bytes + device scan + k_group_offsets chain) -- full GPU suite
-# on it, then A/B on the default C4 line (HBM step, pyflac shim per-stream time, e2e host-band pipeline)
-# and on the 8-way C4 / C3 shares, 3 alternating reps each.
+# v24: the HEAD measurement set (product build after the v22/v23 A/Bs were dropped): full GPU suite,
+# the default C4 bench line (all legs), C3 and C5 with counters + timed kernel stats, the shard projections.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r03}
@@ -11,16 +9,18 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo TESTS_FAILED; grep -E "FAIL|Error|error" $OUT/pytest.log | head; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-FRA_CHAIN1=0 timeout -k 10 400 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_host.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_chain0.log 2>&1 || { echo TESTS0_FAILED; tail -30 $OUT/pytest_chain0.log; exit 1; }
-tail -1 $OUT/pytest_chain0.log
-full() {  # chain1_max
-  FRA_CHAIN1=$1 timeout -k 10 400 python -u bench.py --no-cpu --no-pmc --no-trace > $OUT/b.json 2> $OUT/b.err || { echo BENCH_FAILED $1; tail -20 $OUT/b.err; exit 1; }
-  python -c "import json; d=json.loads(open('$OUT/b.json').read().strip().splitlines()[-1]); print('c4 chain1=%-5s %9.1f MPix/s %7.4f ms  shim %.3f ms/stream  e2e %.2f ms' % ('$1', d['value'], d['ms_per_step'], d['pyflac_shim_c2']['ms_per_stream'], d['e2e']['ms']), d['roofline']['kernel_ms_per_launch'])" | tee -a $OUT/ab.txt
-}
-shard() {  # chain1_max cfg r/N
-  FRA_CHAIN1=$1 timeout -k 10 300 python -u bench.py --config $2 --shard $3 --no-cpu --no-e2e --no-pmc --no-trace > $OUT/b.json 2> $OUT/b.err || { echo SHARD_FAILED $1 $2; tail -20 $OUT/b.err; exit 1; }
-  python -c "import json; d=json.loads(open('$OUT/b.json').read().strip().splitlines()[-1]); print('%s %s chain1=%-5s %8.4f ms/step' % ('$2', '$3', '$1', d['ms_per_step']), d['kernel_ms_per_launch'])" | tee -a $OUT/ab.txt
-}
-for rep in 1 2 3; do full 4096; full 0; done
-for rep in 1 2 3; do shard 4096 c4 4/8; shard 0 c4 4/8; shard 4096 c3 0/8; shard 0 c3 0/8; done
+export FRA_PROF_DIR=$OUT/prof
+timeout -k 10 420 python -u bench.py > $OUT/c4.json 2> $OUT/c4.err || { echo BENCH_C4_FAILED; tail -20 $OUT/c4.err; exit 1; }
+for cfg in c3 c5; do
+timeout -k 10 420 python -u bench.py --config $cfg --no-cpu --no-e2e > $OUT/$cfg.json 2> $OUT/$cfg.err || { echo BENCH_FAILED $cfg; tail -20 $OUT/$cfg.err; exit 1; }
+done
+unset FRA_PROF_DIR
+for cfg in c4 c3 c5; do
+python -c "import json; d=json.loads(open('$OUT/$cfg.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], r['kernel_ms_per_launch'], r['frac'], r['valu_issue_frac'], (r['counters'] or {}).get('stalls'))"
+done
+for sh in c4:0/2 c4:0/4 c4:4/8 c3:0/8 c5:0/8; do
+  cfg=${sh%%:*}; r=${sh#*:}
+  timeout -k 10 300 python -u bench.py --config $cfg --shard $r --no-cpu --no-e2e --no-pmc --no-trace > $OUT/shard.json 2> $OUT/shard.err || { echo SHARD_FAILED $sh; tail -20 $OUT/shard.err; exit 1; }
+  tail -1 $OUT/shard.json >> $OUT/shard.txt
+done
 echo ALLOK
