@@ -34,8 +34,6 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
-hipError_t launch_frame_chain1(const JobArgs& a, unsigned long long* gbase, int grp, int last, hipStream_t s,
-                               unsigned long long* host_mirror);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
@@ -872,22 +870,15 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     st = pack_st;
     pack_st = nullptr;
   }
-  // groups of <= FRA_CHAIN1 frames (default 4096; 0 = off): the chain as one single-workgroup launch
-  static const int chain1_max = getenv("FRA_CHAIN1") ? atoi(getenv("FRA_CHAIN1")) : 4096;
-  if (nf <= chain1_max) {
-    if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));  // the previous group's gbase is read up front
-    HIPCHK(launch_frame_chain1(ga, p->d_gbase, gi, gi == ng - 1, st, host_mirror));
-  } else {
-    HIPCHK(launch_frame_bytes(ga, st));
-    if (nf > 0) {
-      size_t tb = p->scan_stride;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)(slot < 0 ? gi : slot) * p->scan_stride,
-                                              tb, p->d_fbytes + gr.f0, p->d_foff + gr.f0, nf, st));
-    }
-    if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
-    HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
-                                a.nframes_total, st, host_mirror));
+  HIPCHK(launch_frame_bytes(ga, st));
+  if (nf > 0) {
+    size_t tb = p->scan_stride;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)(slot < 0 ? gi : slot) * p->scan_stride, tb,
+                                            p->d_fbytes + gr.f0, p->d_foff + gr.f0, nf, st));
   }
+  if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
+  HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
+                              a.nframes_total, st, host_mirror));
   if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
   if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
   if (pack_st) {  // assembly on the pack stream once this group's offsets exist

@@ -173,8 +173,10 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
   }
 }
 
-// frame g's header (+ CRC-8) and blob bounds -> fmeta[g], its byte size -> frame_bytes[g] (returned)
-__device__ __forceinline__ unsigned long long frame_bytes_of(const JobArgs& a, const int g) {
+__global__ void k_frame_bytes(JobArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.frame_count) return;
+  const int g = a.frame_base + i;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   // FRA-1 3.1b: a mid-side stream keeps the first minimum of L+R, L+S, S+R, M+S (virtual channels 0..3)
@@ -214,65 +216,7 @@ __device__ __forceinline__ unsigned long long frame_bytes_of(const JobArgs& a, c
     if (c < st.channels) bits += a.sf[(size_t)g * a.cmax + vc].bits;
     m[kHdrWords + 2 + c] = c < st.channels ? bits : 0xFFFFFFFFu;
   }
-  const unsigned long long fb = ((uint64_t)(bits + 7) >> 3) + 2;
-  a.frame_bytes[g] = fb;
-  return fb;
-}
-__global__ void k_frame_bytes(JobArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.frame_count) (void)frame_bytes_of(a, a.frame_base + i);
-}
-
-// The whole frame-size chain of a small frame group in ONE launch (one 1024-thread workgroup): frame sizes,
-// the group's exclusive scan (wave scans by shuffles + the 16 wave totals in LDS, carried across rounds of
-// 1024 frames) and the global offsets -- the same outputs as k_frame_bytes + the device scan +
-// k_group_offsets (frame_off[f0 + i] = base + exclusive sum, gbase[grp + 1], frame_off[nframes] of the last
-// group, the page-locked host mirror), four launches fewer on the short plans whose execute is launch-bound
-// (the pyflac-compatible shim, host-pipeline bands, multi-GPU shares).
-__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int d) {
-  const uint32_t lo = __shfl_up((uint32_t)v, d, 64), hi = __shfl_up((uint32_t)(v >> 32), d, 64);
-  return ((unsigned long long)hi << 32) | lo;
-}
-__global__ void __launch_bounds__(1024) k_frame_chain1(JobArgs a, unsigned long long* gbase, int grp, int last,
-                                                       unsigned long long* host_mirror) {
-  __shared__ unsigned long long wsum[16];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  unsigned long long carry = grp == 0 ? 0ull : gbase[grp];
-  for (int i0 = 0; i0 < a.frame_count; i0 += 1024) {
-    const int i = i0 + t;
-    const unsigned long long v = i < a.frame_count ? frame_bytes_of(a, a.frame_base + i) : 0ull;
-    unsigned long long x = v;  // inclusive scan inside the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const unsigned long long y = shfl_up_u64(x, d);
-      if (lane >= d) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    unsigned long long pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const unsigned long long s = wsum[k];
-      pre += k < w ? s : 0ull;
-      tot += s;
-    }
-    if (i < a.frame_count) a.frame_off[a.frame_base + i] = carry + pre + x - v;
-    carry += tot;
-    __syncthreads();  // wsum is rewritten by the next round
-  }
-  if (t == 0) {
-    gbase[grp + 1] = carry;
-    if (last) a.frame_off[a.nframes_total] = carry;
-    if (host_mirror) {
-      host_mirror[grp + 1] = carry;
-      __threadfence_system();
-    }
-  }
-}
-hipError_t launch_frame_chain1(const JobArgs& a, unsigned long long* gbase, int grp, int last, hipStream_t s,
-                               unsigned long long* host_mirror) {
-  k_frame_chain1<<<1, 1024, 0, s>>>(a, gbase, grp, last, host_mirror);
-  return hipGetLastError();
+  a.frame_bytes[g] = ((uint64_t)(bits + 7) >> 3) + 2;
 }
 
 // ============================================================================ launchers
