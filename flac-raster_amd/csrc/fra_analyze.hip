@@ -545,27 +545,7 @@ __device__ void verbatim_to_slot(uint32_t* slot, const SmpT* smp, int n, uint32_
                                  int t) {
   for (uint32_t j = t; j < nw; j += kThreads) slot[j] = verbatim_word(smp, n, hdr, w, sbps, j);
 }
-#ifndef FRA_KEEP
-#define FRA_KEEP 1      // keep the last LPC model's residuals in registers for the winner's encode
-#endif
-#ifndef FRA_FASTLOAD
-#define FRA_FASTLOAD 1  // full-frame LUT load path (load_lut_full)
-#endif
-#ifndef FRA_WAVES16
-#define FRA_WAVES16 6   // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
-#endif
-#ifndef FRA_ANA_SGPR
-// SGPR cap (0 = compiler default; in effect on the 16-bit lag <= 8 instances, the others keep 106).  A
-// SIMD holds 800 SGPRs, allocated per wave as ceil(n/16)*16 + 16 (MI355X_MICROARCH.md, workgroup
-// dispatch): at the default 106 six analysis waves take 768 and no background wave (k_minmax_vec,
-// k_assemble_bg of the pipelined execute) fits beside them; at <= 94 they take 672 (the compiler keeps
-// the excess in VGPR lanes, still 80 VGPRs).  Off by default: the co-resident background assembly it
-// enables was slower on 16-bit plans and the cap costs the analysis ~1 %
-#define FRA_ANA_SGPR 0
-#endif
-#ifndef FRA_PRIO
-#define FRA_PRIO 0  // s_setprio level of the single-wave phases (0 = off)
-#endif
+constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (register budget 512 / waves)
 #ifndef FRA_PREFETCH
 // 16-bit full frames: one wave touches, during the Levinson-Durbin phase, the raw rows of the subframe
 // FRA_PREFETCH workgroups ahead in dispatch order (a multiple of 8: the same XCD, blocks being dealt
@@ -599,8 +579,7 @@ __device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {
 }
 
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : FRA_WAVES16))
-__attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
@@ -646,14 +625,12 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
     FRA_LOAD_STAMP(11, (int)np.mn + st.width + fr.n)
     bool done = false;
     if constexpr (!B32) {
-      if (FRA_FASTLOAD && lut && a.vec8 && a.off32 && n == kMaxBlock) {
+      if (lut && a.vec8 && a.off32 && n == kMaxBlock) {
         done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
         pf_ok = done;
       }
     }
-#ifndef FRA_ONLYFAST
     if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
-#endif
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -755,19 +732,6 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
   }
   FRA_STOP(9)
   FRA_STAMP(2)
-#if defined(FRA_EXP_PAD) && FRA_EXP_PAD > 0
-  {  // diagnostic build: FRA_EXP_PAD extra independent VALU instructions per wave (4 chains of v_add_u32)
-    uint32_t p0 = t, p1 = t + 1, p2 = t + 2, p3 = t + 3;
-#pragma unroll
-    for (int k = 0; k < FRA_EXP_PAD / 4; k++) {
-      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p0) : "v"(p1));
-      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p1) : "v"(p2));
-      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p2) : "v"(p3));
-      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p3) : "v"(p0));
-    }
-    if ((p0 ^ p1 ^ p2 ^ p3) == 0x7FFFFFF3u) S.ired[0][3] = 1;  // keep the chains alive
-  }
-#endif
   const int lmax = cfg.max_lpc < n - 1 ? cfg.max_lpc : n - 1;
   // FIXED models searched during window 0's Levinson-Durbin (psum complete at its barrier)
   const bool early = fixfast && MAXLAG > 0 && cfg.nsub > 0 && lmax > 0;
@@ -867,9 +831,6 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
         if (rw == nldw) { FRA_ROLE_STAMP(16) } else { FRA_ROLE_STAMP(17) }
       }
       if (rw < nldw) {
-        // the Levinson-Durbin wave is the pole of this phase (r03 v18 stamps): FRA_PRIO raises its issue
-        // priority over the other waves of its SIMD for the recursion
-        if (FRA_PRIO) __builtin_amdgcn_s_setprio(FRA_PRIO);
         const int gw = lane >> 4, lo = lane & 15;
         const int wi = 4 * rw + gw;
         const bool gon = wi < a.nwin;
@@ -917,7 +878,6 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
 #pragma unroll
           for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
         }
-        if (FRA_PRIO) __builtin_amdgcn_s_setprio(0);
         FRA_ROLE_STAMP(15)
       }
     }
@@ -980,7 +940,7 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       if constexpr (B32) {
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
       } else {
-        keep_m = FRA_KEEP ? m : -1;
+        keep_m = m;
       }
     }
   } else {
@@ -1026,7 +986,6 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
   }
   for (int m = (early ? 5 : 0) + rw; m < nmod; m += 4) {
     if (!S.mvalid[m] || (m < 5 && m != fg1 && m != fg2)) continue;
-    if (FRA_PRIO) __builtin_amdgcn_s_setprio(FRA_PRIO);  // (single-wave pole, as the LD above)
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
@@ -1036,7 +995,6 @@ __attribute__((amdgpu_num_sgpr(FRA_ANA_SGPR))) k_analyze(JobArgs a, int src) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
     }
-    if (FRA_PRIO) __builtin_amdgcn_s_setprio(0);
     FRA_ROLE_STAMP(18)
   }
   {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share
@@ -1583,13 +1541,7 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-#ifdef FRA_EXP_LDS
-  // diagnostic build: FRA_EXP_LDS=bytes of dynamic LDS per workgroup (lowers the workgroups per CU)
-  static const unsigned dyn = getenv("FRA_EXP_LDS") ? (unsigned)atoi(getenv("FRA_EXP_LDS")) : 0u;
-#else
-  constexpr unsigned dyn = 0;
-#endif
-#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, dyn, s>>>(a, src)
+#define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
   if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one
     grid.y = 2;

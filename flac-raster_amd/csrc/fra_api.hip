@@ -682,9 +682,7 @@ static int plan_build(fra_plan* p) {
         HIPCHK(hipStreamCreateWithPriority(&p->pack, hipStreamNonBlocking, lo));
         // 16-bit plans: C4 -1.2 %, C3 -2.4 %; 32-bps plans keep one analysis stream (C5 +5 %: the early
         // start takes the slots the background assembly was using) (r03 v14)
-        static const int dual_env = getenv("FRA_DUAL_ANA") ? atoi(getenv("FRA_DUAL_ANA")) : -1;
-        const bool dual = dual_env < 0 ? !p->b32 : dual_env != 0;
-        if (dual)
+        if (!p->b32)
           for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
       }
       for (int b = 0; b < 2; b++) {
@@ -710,13 +708,10 @@ static void use_buffers(fra_plan* p, int b) {
   p->cur = b;
 }
 // the pipelined execute's assembly kernel: k_assemble_bg (<= 32 VGPRs, one workgroup per CU) on 32-bps
-// plans, whose four analysis workgroups per CU leave room for it; k_assemble on 16-bit plans, where the
-// background form did not fit beside six analysis workgroups (SGPRs) and, made to fit (FRA_ANA_SGPR=94),
-// was slower than the per-frame grid (r03 v7/v8).  FRA_PIPE_ASM=0 / 1 forces k_assemble / k_assemble_bg.
-static bool pipe_asm_bg(const fra_plan* p) {
-  static const int m = getenv("FRA_PIPE_ASM") ? atoi(getenv("FRA_PIPE_ASM")) : -1;
-  return m < 0 ? p->b32 : m == 1;
-}
+// plans, whose four analysis workgroups per CU leave room for it; k_assemble4 on 16-bit plans, where the
+// background form did not fit beside the analysis (SGPRs) and, made to fit, was slower than the per-frame
+// grid (r03 v7/v8)
+static bool pipe_asm_bg(const fra_plan* p) { return p->b32; }
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
   if (!p->pipe) return FRA_OK;
@@ -841,9 +836,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
     // background norm stage: one workgroup per CU striding over the row blocks (it shares the CUs with
     // k_analyze instead of filling them)
-    static const int bg_blocks = getenv("FRA_BG_BLOCKS") ? atoi(getenv("FRA_BG_BLOCKS")) : -1;
-    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, nst_s,
-                         norm_st ? (bg_blocks >= 0 ? bg_blocks : p->ncu) : 0));
+    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, nst_s, norm_st ? p->ncu : 0));
     HIPCHK(launch_norm_finalize(ma, nc, nst_s));
     HIPCHK(launch_norm_lut(p->src, ma, nc, nst_s));
   }
@@ -860,11 +853,10 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
   // pipelined execute: the frame-size chain (k_frame_bytes, scan, k_group_offsets) only feeds this
   // execute's assembly, so it goes onto the pack stream with it and the plan's stream proceeds straight to
-  // the next execute's analysis (FRA_CHAIN_BG=0: the chain stays on the plan's stream)
-  static const bool chain_bg = !(getenv("FRA_CHAIN_BG") && atoi(getenv("FRA_CHAIN_BG")) == 0);
+  // the next execute's analysis
   // background form of k_assemble (<= 32 VGPRs, ~one workgroup per CU) beside the next execute's analysis
   const int bg_blocks = (pack_st && pipe_asm_bg(p)) ? p->ncu : 0;
-  if (pack_st && chain_bg && !ev_prev && !ev_pub && !host_mirror) {
+  if (pack_st && !ev_prev && !ev_pub && !host_mirror) {
     HIPCHK(hipEventRecord(ev_scan, st));
     HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
     st = pack_st;
@@ -1048,9 +1040,12 @@ int fra_plan_timing(fra_plan* p, float* ms4, int32_t* n) {
 int fra_plan_set_first_frame(fra_plan* p, int32_t first_frame) {
   if (!p || first_frame < 0) return set_err(FRA_E_INVALID, "bad argument");
   (void)hipSetDevice(p->ctx->device);
+  // pipelined executes still in flight read frame_number0 on the analysis / pack streams (k_frame_bytes):
+  // let them finish before the table changes under them
+  if (int rc = plan_sync_all(p)) return rc;
   p->job.first_frame = first_frame;
   for (auto& st : p->streams) st.frame_number0 = (uint32_t)first_frame;
-  if (!p->streams.empty())  // ordered before the next execute on the plan's stream
+  if (!p->streams.empty())  // complete before this call returns, so every later execute reads it
     HIPCHK(hipMemcpyAsync(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(),
                           hipMemcpyHostToDevice, p->ctx->stream));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));  // the host array may change again before it is read

@@ -1,5 +1,5 @@
-// fra_assemble.h -- frame assembly + CRC-16 of one frame by one workgroup (device code), shared by
-// k_assemble / k_assemble_bg (fra_pack.hip) and the fused assembly tail of k_analyze (fra_analyze.hip).
+// fra_assemble.h -- frame assembly + CRC-16 of one frame by one wave (device code) for k_assemble4 and
+// k_assemble_bg (fra_pack.hip).
 //
 // Emits what libFLAC's frame writer emits for every 4,096-sample block that
 // FLAC__stream_encoder_process_interleaved / _finish produce under the pyflac calls at
@@ -36,7 +36,7 @@ __device__ int g_guard_count;
 #define GUARD(cond, ...) do {} while (0)
 #endif
 
-constexpr int kMLo = 4, kMLevels = 9;  // LDS copy of multiply tables x^(8*2^i), i = 4..12
+constexpr int kMLo = 4, kMLevels = 7;  // LDS copy of multiply tables x^(8*2^i), i = 4..10
 
 // multiply a CRC-16 remainder by the constant of table m (512 entries): two byte-table lookups
 __device__ __forceinline__ uint32_t crc_mul_tab(const uint16_t* m, uint32_t c) {
@@ -60,18 +60,16 @@ __device__ __forceinline__ uint32_t gf16_mul_dev(uint32_t a, uint32_t b) {
 
 struct alignas(16) AssembleSmem {
   uint16_t T[16][256];  // slice-by-16: T[k][v] = CRC of v followed by k zero bytes
-  uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..12 (tree 4..9, waves 10..11, Horner 12)
+  uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..10 (tree 4..9, Horner 10)
   uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_bytes); [wave]
-  uint32_t crcw[4];
   uint32_t tailw[4];    // the output window of the last, partial dword (bytes [4*NF - A, L)); [wave]
 };
 // background form: only the per-quad tables in LDS (9.3 KiB: it fits beside four 32-bps k_analyze
 // workgroups too); the once-per-frame tree levels 4..11 are read from global memory (L1/L2 resident)
 struct alignas(16) AssembleSmemBg {
   uint16_t T[16][256];
-  uint16_t Mh[512];     // the Horner step: x^(8*2^12) (a frame per workgroup) or x^(8*2^10) (per wave)
+  uint16_t Mh[512];     // the Horner step x^(8*2^10)
   uint32_t meta[4][kMetaWords];
-  uint32_t crcw[4];
   uint32_t tailw[4];
 };
 
@@ -86,11 +84,11 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 }
 
 // CRC tables to LDS (16-byte loads) so no step of the CRC chain waits on a global gather
-template <typename SM, int NT = kThreads>
+template <typename SM>
 __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
   constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
   const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
-  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kBg ? (NT == 64 ? 10 : 12) : kMLo) * 512);
+  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kBg ? 10 : kMLo) * 512);
   uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
   uint4* dM;
   if constexpr (kBg) dM = reinterpret_cast<uint4*>(&S.Mh[0]);
@@ -102,27 +100,25 @@ __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
   }
 }
 
-// one frame by NT threads -- the whole workgroup (NT = 256) or one wave (NT = 64: four frames per
-// workgroup, no workgroup barrier per frame, the CRC tables copied once for the four) -- U quads per
-// thread per round.  Header and blob bounds come precomputed from k_frame_bytes, so every metadata load is
-// issued in the first round; TABLES (NT = 256): the CRC tables are copied here, while the first slot loads
-// are in flight (one workgroup per frame)
-template <int U, bool TABLES, typename SM, int NT = kThreads>
+// one frame by one wave (four frames per workgroup, no workgroup barrier per frame, the CRC tables copied
+// to LDS once for the four by the caller), U quads per lane per round.  Header and blob bounds come
+// precomputed from k_frame_bytes, so every metadata load is issued in the first round
+template <int U, typename SM>
 __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM& S) {
-  static_assert(NT == kThreads || NT == 64, "a frame per workgroup or per wave");
+  constexpr int NT = 64;  // lanes per frame
   const int lane = (int)threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int t = NT == 64 ? lane : (int)threadIdx.x;  // thread index within the frame's group
+  const int t = lane;
   constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
-  uint32_t* const meta = S.meta[NT == 64 ? wv : 0];
-  uint32_t& tailw = S.tailw[NT == 64 ? wv : 0];
-  const uint16_t* M;     // tree / wave levels kMLo..11
-  const uint16_t* Mh;    // the Horner level: x^(128 NT) = x^(8 * 2^12) (NT = 256) or x^(8 * 2^10) (NT = 64)
-  if constexpr (kBg) {  // (copy_tables<SM, NT> put the matching Horner level in S.Mh)
+  uint32_t* const meta = S.meta[wv];
+  uint32_t& tailw = S.tailw[wv];
+  const uint16_t* M;     // tree levels kMLo..9
+  const uint16_t* Mh;    // the Horner level: x^(128 NT) = x^(8 * 2^10)
+  if constexpr (kBg) {  // (copy_tables<SM> put the Horner level in S.Mh)
     M = a.crctab + 1024 + kMLo * 512;
     Mh = &S.Mh[0];
   } else {
     M = &S.M[0][0];
-    Mh = &S.M[(NT == 64 ? 10 : 12) - kMLo][0];
+    Mh = &S.M[10 - kMLo][0];
   }
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
@@ -239,16 +235,12 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   };
   uint32_t wn[U][5], shn[U];
   if (q0 < NQW) fetch(q0, wn, shn);
-  // CRC tables and header words to LDS while the first slot loads are in flight
-  if constexpr (TABLES) copy_tables(a, S);
+  // header words to LDS while the first slot loads are in flight
   if (t < kMetaWords) meta[t] = a.fmeta[(size_t)g * kMetaWords + t];
-  if constexpr (NT == 64) {  // this wave's LDS stores -> its own reads
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-  } else {
-    __syncthreads();
-  }
+  // this wave's LDS stores -> its own reads
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
   for (; q0 < NQW; q0 += NT * U) {
     uint32_t w[U][5], sh[U];
 #pragma unroll
@@ -321,25 +313,12 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   acc ^= crc_mul(M, 7, dpp32<DPP_SHR8, 0xF>(acc));
   acc ^= crc_mul(M, 8, dpp32<DPP_BC15, 0xA>(acc));
   acc ^= crc_mul(M, 9, dpp32<DPP_BC31, 0xC>(acc));
-  bool last;  // the thread that finishes the frame
-  uint32_t crc;
-  if constexpr (NT == 64) {  // the wave's accumulators are the frame's: lane 63 holds the CRC
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // tailw (any lane) -> lane 63
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-    last = lane == 63;
-    crc = acc;
-  } else {
-    if (lane == 63) S.crcw[wv] = acc;
-    __syncthreads();
-    last = t == 0;
-    if (last) {
-      const uint32_t c01 = crc_mul(M, 10, S.crcw[0]) ^ S.crcw[1];
-      const uint32_t c23 = crc_mul(M, 10, S.crcw[2]) ^ S.crcw[3];
-      crc = crc_mul(M, 11, c01) ^ c23;
-    }
-  }
-  if (last) {
+  // the wave's accumulators are the frame's: lane 63 holds the CRC
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // tailw (any lane) -> lane 63
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t crc = acc;
+  if (lane == 63) {
     // remove the e zero dwords that followed dword NF-1 inside the last CRC quad: * x^(-32e)
     const int e = (int)(4 * NQ - (NF + a4));
     constexpr uint32_t kInvX32[4] = {0x0001u, 0xCAA8u, 0x25DDu, 0x37B1u};  // x^(-32e) mod P

@@ -1,23 +1,12 @@
-// fra_pack.hip -- the frame assembly kernels (one frame per workgroup; the per-frame device code, its
-// gather formulation and the CRC-16 scheme are in fra_assemble.h):
-// * k_assemble4 (default: one frame per wave, four per workgroup) / k_assemble (one per workgroup);
-// * k_assemble_bg: background form (see below);
-// * the pipelined execute fuses the assembly of execute k into the tail of execute k+1's k_analyze.
+// fra_pack.hip -- the frame assembly kernels (the per-frame device code, its gather formulation and the
+// CRC-16 scheme are in fra_assemble.h), both one frame per wave:
+// * k_assemble4: four frames per workgroup (serial executes, and pipelined 16-bit plans on the pack stream);
+// * k_assemble_bg: background form for pipelined 32-bps plans (see below).
 #include <cstdlib>
 
 #include "fra_assemble.h"
 
-#ifndef FRA_BG_PER_WAVE
-#define FRA_BG_PER_WAVE 1
-#endif
-
 namespace fra {
-
-// one workgroup per frame (FRA_ASM_WAVE=0; the r02 form)
-__global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
-  __shared__ AssembleSmem S;
-  assemble_frame<2, true>(a, a.frame_base + (int)blockIdx.x, S);
-}
 
 // background form for the pipelined execute, where it runs beside the next execute's k_analyze: a
 // k_analyze<16-bit> CU holds 6 workgroups of 80 VGPRs and <= 94 SGPRs per wave, leaving per SIMD 32 VGPRs
@@ -29,20 +18,12 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble(JobArgs a) {
 __global__ void __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_num_vgpr(16),
                                amdgpu_num_sgpr(96))) k_assemble_bg(JobArgs a) {
   __shared__ AssembleSmemBg S;
-#if FRA_BG_PER_WAVE
   // one frame per wave, each wave striding over the frames on its own (no workgroup barrier per frame)
-  copy_tables<AssembleSmemBg, 64>(a, S);
+  copy_tables(a, S);
   __syncthreads();
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   for (int i = (int)blockIdx.x * 4 + w; i < a.frame_count; i += (int)gridDim.x * 4)
-    assemble_frame<1, false, AssembleSmemBg, 64>(a, a.frame_base + i, S);
-#else
-  copy_tables(a, S);
-  for (int i = (int)blockIdx.x; i < a.frame_count; i += (int)gridDim.x) {
-    __syncthreads();  // the previous frame's readers of S.meta / S.crcw / S.tailw are done
-    assemble_frame<1, false>(a, a.frame_base + i, S);
-  }
-#endif
+    assemble_frame<1>(a, a.frame_base + i, S);
 }
 
 // the default: four frames per workgroup, one per wave -- the 17.5 KiB of CRC tables are copied to LDS
@@ -54,17 +35,13 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble4(JobArgs a) {
   copy_tables(a, S);
   __syncthreads();
   const int i = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  if (i < a.frame_count) assemble_frame<2, false, AssembleSmem, 64>(a, a.frame_base + i, S);
+  if (i < a.frame_count) assemble_frame<2>(a, a.frame_base + i, S);
 }
 
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks) {
   if (a.frame_count <= 0) return hipSuccess;
   if (bg_blocks > 0) k_assemble_bg<<<(unsigned)std::min(bg_blocks, a.frame_count), kThreads, 0, s>>>(a);
-  else {
-    static const bool per_wg = getenv("FRA_ASM_WAVE") && atoi(getenv("FRA_ASM_WAVE")) == 0;
-    if (per_wg) k_assemble<<<(unsigned)a.frame_count, kThreads, 0, s>>>(a);  // one frame per workgroup
-    else k_assemble4<<<(unsigned)((a.frame_count + 3) / 4), kThreads, 0, s>>>(a);
-  }
+  else k_assemble4<<<(unsigned)((a.frame_count + 3) / 4), kThreads, 0, s>>>(a);
   return hipGetLastError();
 }
 

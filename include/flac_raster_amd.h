@@ -140,7 +140,8 @@ FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_
  * thread fills host_raster top to bottom, cli.py:553-559 reads each tile's window before its encode):
  * before the H2D copy of a row band is enqueued, the call waits until *rows_ready >= the band's last row
  * + 1 (the producer publishes rows with a release store; -1 = the producer failed: FRA_E_STATE).  Rows
- * are image rows of the job's raster (row_stride units). */
+ * are image rows of the job's raster (row_stride units).  Contract: the producer MUST eventually publish
+ * either every row or -1 (also when it fails or is cancelled); the call waits without a time limit. */
 FRA_API int fra_plan_encode_host_progress(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
                                           uint64_t *total_bytes, const volatile int64_t *rows_ready);
 /* frame number of every stream's first frame for the next execute (the job's first_frame until set) */
