@@ -69,8 +69,6 @@ constexpr int buf_words() { return B32 ? kMaxBlock + 16 : kMaxBlock / 2 + 16; }
 //   read_x28: x[j] = sample 16t - 12 + j (the previous chunk's last 12, the zero chunk for t = 0)
 //   read_y24: y[j] = sample 16t + j, j < 24 (this chunk + the next chunk's first 8)
 // int16 storage is read as aligned dword pairs and sign-extended (2 samples per ds_read lane-dword)
-__device__ __forceinline__ int32_t lo16(uint32_t v) { return (int32_t)(int16_t)(v & 0xFFFFu); }
-__device__ __forceinline__ int32_t hi16(uint32_t v) { return (int32_t)v >> 16; }
 __device__ __forceinline__ void read_x28(const int32_t* smp, int t, int32_t (&x)[28]) {
 #pragma unroll
   for (int j = 0; j < 12; j++) x[j] = smp[t * kSmpStride + 4 + j];
@@ -114,20 +112,6 @@ __device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)
   }
 }
 
-// apodization coefficients of samples i0 .. i0 + 16 + MAXLAG - 1 of one window (row of the plan's window
-// table, exactly n entries used): unconditional vector loads when the whole span lies inside the block,
-// else only the entries below n (the others are never multiplied: wf = 0 past n) -- no read past the
-// window the frame owns (the table is allocated at its exact size)
-template <int MAXLAG>
-__device__ __forceinline__ void load_window(const float* win, int i0, int n, float (&w)[kChunk + MAXLAG]) {
-  if (i0 + kChunk + MAXLAG <= n) {
-#pragma unroll
-    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = win[i0 + j];
-  } else {
-#pragma unroll
-    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = i0 + j < n ? win[i0 + j] : 0.0f;
-  }
-}
 
 // windows per block at this lag bound (levels 3-6: <= 3 with max_lpc 8; levels 7-8: <= 6)
 template <int MAXLAG>
@@ -236,10 +220,6 @@ __device__ __forceinline__ uint64_t lpc_abs2_f64(const double* xd, const double*
 // 16-bit path LPC predictor with v_dot2c_i32_i16: samples fit int16 and |q| < 2^11, so the pairwise
 // int16 products accumulate exactly in int32 (|sum| < 12 * 2^26); q pairs Q[p] = (q[2p], q[2p+1]),
 // sample pairs A(m) = (x[m], x[m-1]) -> pred(b) = sum_p dot2(A(b - 1 - 2p), Q[p])
-typedef short fra_short2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ fra_short2 pack_pair(int32_t lo, int32_t hi) {
-  return __builtin_bit_cast(fra_short2, __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u));
-}
 template <int NP>
 __device__ __forceinline__ int32_t pred_dot2(const int32_t* x, int b, const fra_short2 (&Q)[NP]) {
   int32_t acc = 0;
@@ -262,26 +242,6 @@ __device__ __forceinline__ void read_d14(const int16_t* smp, int t, uint32_t (&D
   for (int j = 0; j < 6; j++) D[j] = d[(t * kSmpStride + 4) / 2 + j];
 #pragma unroll
   for (int j = 0; j < 8; j++) D[6 + j] = d[(t + 1) * kSmpStride / 2 + j];
-}
-__device__ __forceinline__ uint32_t pair_at(const uint32_t (&D)[14], int k) {
-  return (k & 1) ? __builtin_amdgcn_alignbit(D[(k + 1) >> 1], D[(k - 1) >> 1], 16) : D[k >> 1];
-}
-__device__ __forceinline__ int32_t sample_at(const uint32_t (&D)[14], int k) {
-  return (k & 1) ? hi16(D[k >> 1]) : lo16(D[k >> 1]);
-}
-template <int NP>
-__device__ __forceinline__ void q_pairs_rev(const int32_t* q, fra_short2 (&Q)[NP]) {
-#pragma unroll
-  for (int p = 0; p < NP; p++) Q[p] = pack_pair(q[2 * p + 1], q[2 * p]);
-}
-// prediction of x[b]: sum_p dot2((x[b-2-2p], x[b-1-2p]), (q[2p+1], q[2p]))
-template <int NP>
-__device__ __forceinline__ int32_t pred_raw(const uint32_t (&D)[14], int b, const fra_short2 (&Q)[NP]) {
-  int32_t acc = 0;
-#pragma unroll
-  for (int p = 0; p < NP; p++)
-    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(fra_short2, pair_at(D, b - 2 - 2 * p)), Q[p], acc, false);
-  return acc;
 }
 // sum of |residual| of order O over the thread's 16 samples (warm-up positions jj < O of thread 0 masked),
 // the residuals kept in r for the winner's encode
@@ -585,7 +545,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
   // 7-wave 16-bit instance
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int g = a.frame_base + (int)blockIdx.x;
+  const int g = a.flist ? a.flist[blockIdx.x] : a.frame_base + (int)blockIdx.x;
   // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the
   // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
   // the encoder's scan) keeps the physical wave index wv
@@ -627,7 +587,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
     if constexpr (!B32) {
       if (lut && a.vec8 && a.off32 && n == kMaxBlock) {
         done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
-        pf_ok = done;
+        pf_ok = done && !a.flist;  // (the prefetch target is found by dispatch order)
       }
     }
     if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
@@ -1536,11 +1496,34 @@ extern "C" __attribute__((visibility("default"))) int fra_diag_stamps(void* host
 namespace fra {
 #endif
 
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s) {
+hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s);
+
+// slow != null (16-bit plans whose full frames k_analyze_w takes, fra_api.hip wave_path): k_analyze_w over
+// the launch's frames, then k_analyze over the nslow partial frames slow[0..nslow) of the launch's range
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, const int32_t* slow,
+                          int nslow) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
+  if (slow && !b32) {
+    hipError_t e = launch_analyze_w(src, a.level, a, ms ? 2 : a.cmax, s);
+    if (e != hipSuccess) return e;
+    if (nslow > 0) {
+      JobArgs sa = a;
+      sa.flist = slow;
+      sa.frame_count = nslow;
+      dim3 sg((unsigned)nslow, (unsigned)(ms ? 2 : a.cmax));
+      if (ml == 0) k_analyze<false, 0><<<sg, kThreads, 0, s>>>(sa, src);
+      else k_analyze<false, 8><<<sg, kThreads, 0, s>>>(sa, src);
+    }
+    if (ms) {
+      grid.y = 2;
+      if (ml == 0) k_analyze<true, 0><<<grid, kThreads, 0, s>>>(a, src);
+      else k_analyze<true, 8><<<grid, kThreads, 0, s>>>(a, src);
+    }
+    return hipGetLastError();
+  }
 #define FRA_LAUNCH(B, M) k_analyze<B, M><<<grid, kThreads, 0, s>>>(a, src)
   if (ms && !b32) {
     // mid-side 16-bps plan: L, R on the 16-bit instance, then M and S (17-bit samples) on the 32-bit one

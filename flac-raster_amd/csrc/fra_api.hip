@@ -32,7 +32,8 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
                          hipStream_t s, int max_blocks);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s);
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, const int32_t* slow,
+                          int nslow);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
@@ -91,6 +92,10 @@ struct fra_plan {
   NormDev* d_norm = nullptr;
   float* d_win = nullptr;
   int32_t* d_wrange = nullptr;
+  int32_t* d_wplat = nullptr;
+  // frames whose block is shorter than kMaxBlock (ascending): k_analyze_w takes the full ones
+  std::vector<int32_t> slow;
+  int32_t* d_slow = nullptr;
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -302,6 +307,8 @@ void fra_plan_destroy(fra_plan* p) {
   if (!p->pipe) (void)hipFree(p->d_norm);
   (void)hipFree(p->d_win);
   (void)hipFree(p->d_wrange);
+  (void)hipFree(p->d_wplat);
+  (void)hipFree(p->d_slow);
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
     for (int b = 0; b < 2; b++) {
       (void)hipFree(p->sf2[b]);
@@ -554,6 +561,29 @@ static int plan_build(fra_plan* p) {
       }
     HIPCHK(hipMalloc(&p->d_wrange, sizeof(int32_t) * wr.size()));
     HIPCHK(hipMemcpy(p->d_wrange, wr.data(), sizeof(int32_t) * wr.size(), hipMemcpyHostToDevice));
+    // longest run of coefficients exactly 1.0f (the tukey plateau): its products are the samples themselves
+    std::vector<int32_t> wp(2 * (size_t)nt * nw, 0);
+    for (int t = 0; t < nt; t++)
+      for (int w = 0; w < nw; w++) {
+        const float* o = wt.data() + ((size_t)t * nw + w) * j.blocksize;
+        int best = 0, blo = 0, run = 0;
+        for (int i = 0; i < j.blocksize; i++) {
+          run = o[i] == 1.0f ? run + 1 : 0;
+          if (run > best) { best = run; blo = i + 1 - run; }
+        }
+        wp[2 * ((size_t)t * nw + w)] = blo;
+        wp[2 * ((size_t)t * nw + w) + 1] = blo + best;
+      }
+    HIPCHK(hipMalloc(&p->d_wplat, sizeof(int32_t) * wp.size()));
+    HIPCHK(hipMemcpy(p->d_wplat, wp.data(), sizeof(int32_t) * wp.size(), hipMemcpyHostToDevice));
+  }
+  {
+    p->slow.clear();
+    for (int f = 0; f < nfr; f++)
+      if (p->frames[f].n != kMaxBlock) p->slow.push_back(f);
+    HIPCHK(hipMalloc(&p->d_slow, sizeof(int32_t) * std::max<size_t>(1, p->slow.size())));
+    if (!p->slow.empty())
+      HIPCHK(hipMemcpy(p->d_slow, p->slow.data(), sizeof(int32_t) * p->slow.size(), hipMemcpyHostToDevice));
   }
   if (!p->streams.empty())
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
@@ -627,6 +657,7 @@ static int plan_build(fra_plan* p) {
   a.norm = p->d_norm;
   a.win = p->d_win;
   a.wrange = p->d_wrange;
+  a.wplat = p->d_wplat;
   a.sf = p->d_sf;
   a.frame_bytes = p->d_fbytes;
   a.frame_off = p->d_foff;
@@ -814,6 +845,14 @@ static void collect_times(fra_plan* p) {
   p->pending_times = false;
 }
 
+// k_analyze_w (one subframe per wave, fra_analyze_w.hip) takes the full frames of 16-bit plans normalised
+// through the per-tile table with 8-byte sample vectors at levels 0-6; FRA_ANALYZE_WG=1 keeps every frame on
+// the workgroup kernel (tests compare both)
+static bool wave_path(const fra_plan* p) {
+  const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
+  return !wg && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&
+         p->job.level <= 6;
+}
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
 static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hipStream_t st, hipEvent_t ev_prev,
@@ -848,7 +887,17 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   JobArgs ga = a;
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
-  HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st));
+  {
+    const int32_t* slow = nullptr;
+    int nslow = 0;
+    if (wave_path(p)) {  // k_analyze_w for the full frames, k_analyze for this range's partial ones
+      const auto lo = std::lower_bound(p->slow.begin(), p->slow.end(), gr.f0);
+      const auto hi = std::lower_bound(lo, p->slow.end(), gr.f1);
+      slow = p->d_slow + (lo - p->slow.begin());
+      nslow = (int)(hi - lo);
+    }
+    HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, slow, nslow));
+  }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
   // pipelined execute: the frame-size chain (k_frame_bytes, scan, k_group_offsets) only feeds this

@@ -909,6 +909,52 @@ __device__ __forceinline__ void lds_put_al(uint32_t* buf, uint32_t P, uint32_t c
   atomicOr(&buf[w0 + 1], __builtin_amdgcn_alignbit(cal, 0u, P & 31u));
 }
 
+// ---------------------------------------------------------------- 16-bit sample pairs (k_analyze, k_analyze_w)
+// int16 storage is read as aligned dword pairs and sign-extended (2 samples per dword, even sample low)
+__device__ __forceinline__ int32_t lo16(uint32_t v) { return (int32_t)(int16_t)(v & 0xFFFFu); }
+__device__ __forceinline__ int32_t hi16(uint32_t v) { return (int32_t)v >> 16; }
+typedef short fra_short2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fra_short2 pack_pair(int32_t lo, int32_t hi) {
+  return __builtin_bit_cast(fra_short2, __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u));
+}
+// D[j] = samples (x[2j], x[2j+1]); the dot2 operand pair (x[k], x[k+1]) is a word itself for even k,
+// one v_alignbit for odd k
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&D)[14], int k) {
+  return (k & 1) ? __builtin_amdgcn_alignbit(D[(k + 1) >> 1], D[(k - 1) >> 1], 16) : D[k >> 1];
+}
+__device__ __forceinline__ int32_t sample_at(const uint32_t (&D)[14], int k) {
+  return (k & 1) ? hi16(D[k >> 1]) : lo16(D[k >> 1]);
+}
+template <int NP>
+__device__ __forceinline__ void q_pairs_rev(const int32_t* q, fra_short2 (&Q)[NP]) {
+#pragma unroll
+  for (int p = 0; p < NP; p++) Q[p] = pack_pair(q[2 * p + 1], q[2 * p]);
+}
+// prediction of x[b]: sum_p dot2((x[b-2-2p], x[b-1-2p]), (q[2p+1], q[2p]))
+template <int NP>
+__device__ __forceinline__ int32_t pred_raw(const uint32_t (&D)[14], int b, const fra_short2 (&Q)[NP]) {
+  int32_t acc = 0;
+#pragma unroll
+  for (int p = 0; p < NP; p++)
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(fra_short2, pair_at(D, b - 2 - 2 * p)), Q[p], acc, false);
+  return acc;
+}
+
+// apodization coefficients of samples i0 .. i0 + 16 + MAXLAG - 1 of one window (row of the plan's window
+// table, exactly n entries used): unconditional vector loads when the whole span lies inside the block,
+// else only the entries below n (the others are never multiplied: wf = 0 past n) -- no read past the
+// window the frame owns (the table is allocated at its exact size)
+template <int MAXLAG>
+__device__ __forceinline__ void load_window(const float* win, int i0, int n, float (&w)[kChunk + MAXLAG]) {
+  if (i0 + kChunk + MAXLAG <= n) {
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = win[i0 + j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kChunk + MAXLAG; j++) w[j] = i0 + j < n ? win[i0 + j] : 0.0f;
+  }
+}
+
 // ---------------------------------------------------------------- frame header (RFC 9639 9.1)
 __host__ __device__ inline int utf8_len(uint32_t v) {
   if (v < 0x80) return 1;

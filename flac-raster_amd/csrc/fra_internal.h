@@ -187,6 +187,7 @@ struct JobArgs {
   NormDev* norm;
   const float* win;        // [ntables][nwin][blocksize]
   const int32_t* wrange;   // [ntables][nwin][2]: nonzero extent [lo, hi) of each window
+  const int32_t* wplat;    // [ntables][nwin][2]: the longest run [lo, hi) of coefficients exactly 1.0f
   SfDesc* sf;              // [nframes_total][cmax]
   unsigned long long* frame_bytes;  // [nframes_total + 1] (last = 0)
   unsigned long long* frame_off;  // [nframes_total + 1] exclusive scan of frame_bytes
@@ -208,6 +209,7 @@ struct JobArgs {
                            // (k_analyze fast load path: 32-bit lane offsets from a uniform base)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
+  const int32_t* flist;    // k_analyze only: if set, workgroup x analyses frame flist[x] (frame_count of them)
 };
 
 }  // namespace fra

@@ -246,3 +246,55 @@ def test_two_channel_pyflac_path_mid_side():
     a32 = a.astype(np.int32) * 97  # 32-bps: independent channels only
     info, frames = N.encode_interleaved(a32, 44100, level=5)
     assert frames == O.encode(a32, 44100, level=5, with_header=False)
+
+
+# ---- k_analyze_w (one subframe per wave: full frames of <= 16-bit rasters, levels 0-6)
+@pytest.mark.parametrize("level", [0, 1, 3, 4, 5, 6])
+@pytest.mark.parametrize("dtype", ["uint8", "int16"])
+def test_wave_kernel_levels_dtypes(level, dtype):
+    """Every level the wave kernel takes, both LUT widths, full + partial frames (partial ones go to
+    k_analyze through the frame list) against the oracle."""
+    r = synth_window(4 if dtype == "uint8" else 3, 7 + level, 2, 300, 700).astype(np.float64)
+    info = np.iinfo(dtype)
+    r = np.clip(r / r.max() * (info.max - info.min) + info.min, info.min, info.max).astype(dtype)
+    check_windows(r, [(0, 0, 300, 700), (0, 0, 64, 64), (17, 9, 131, 257)], level, 16)
+
+
+def test_wave_kernel_equals_workgroup_kernel(monkeypatch):
+    """k_analyze_w and k_analyze (FRA_ANALYZE_WG=1) produce the same bytes on a C4-like scene."""
+    H = W = 1300
+    r = synth_window(4, 99, 4, H, W)
+    wins = tiles(H, W, 1024)
+    _, wave = N.encode_windows(r, wins, level=5, norm=16)
+    monkeypatch.setenv("FRA_ANALYZE_WG", "1")
+    _, wg = N.encode_windows(r, wins, level=5, norm=16)
+    assert wave == wg
+
+
+def _noise_then_smooth(n_frames=3, seed=5):
+    """1-band uint16 rows whose frames start with 1024 samples of full-range noise followed by a slow ramp:
+    the first quarter costs ~17 bits/sample, so the encoded bits of chunks 0-63 run past their own sample
+    words in the LDS bit buffer (k_analyze_w encodes such a subframe straight into the slot)."""
+    rng = np.random.default_rng(seed)
+    x = np.empty(4096 * n_frames, np.uint16)
+    for f in range(n_frames):
+        blk = x[4096 * f: 4096 * (f + 1)]
+        blk[:1024] = rng.integers(0, 65536, 1024)
+        blk[1024:] = (np.arange(3072) * 3 + 1000 * f).astype(np.uint16)
+    return x.reshape(1, -1, 4096)
+
+
+@pytest.mark.parametrize("level", [0, 5, 6])
+def test_wave_kernel_incompressible_start(level):
+    r = _noise_then_smooth()
+    check_windows(r, [(0, 0, r.shape[1], 4096)], level, 16)
+
+
+def test_wave_kernel_constant_and_two_valued():
+    """Constant frames (CONSTANT subframes), two-valued frames and their mix in one stream."""
+    base = synth_window(3, 11, 1, 64, 192)[0].astype(np.int64)
+    x = np.empty((1, 64 * 3, 192), np.int16)
+    x[0, :64] = ((base % 4000) * 8 - 16000).astype(np.int16)
+    x[0, 64:128] = 1234
+    x[0, 128:] = np.where(base % 2 == 0, -5, 7).astype(np.int16)
+    check_windows(x, [(0, 0, 64, 192), (64, 0, 64, 192), (128, 0, 64, 192), (0, 0, 192, 192)], 5, 16)
