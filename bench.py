@@ -226,8 +226,17 @@ def inrun_pmc(args, kernel):
                          "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"], "valu")
     gr = pmc_pass(args, ["SQ_WAVES", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT",
                          "GRBM_GUI_ACTIVE"], "grbm")
-    if fe and wr and kernel in fe and kernel in wr:
-        res["traffic"] = int(2 * _med(fe[kernel]["FETCH_SIZE"]) * 1024 + _med(wr[kernel]["WRITE_SIZE"]) * 1024)
+    # the analysis phase is k_analyze_w (full frames, one subframe per wave) + k_analyze (partial frames)
+    # on 16-bit LUT plans, k_analyze alone otherwise: traffic summed over the phase's kernels, the per-wave
+    # counters of the larger one
+    group = [kernel]
+    if kernel == "k_analyze" and va and "k_analyze_w" in va:
+        group = ["k_analyze_w", "k_analyze"]
+        kernel = "k_analyze_w"
+        res["kernels"] = group
+    if fe and wr and all(k in fe and k in wr for k in group if k in fe):
+        res["traffic"] = int(sum(2 * _med(fe[k]["FETCH_SIZE"]) * 1024 + _med(wr[k]["WRITE_SIZE"]) * 1024
+                                 for k in group if k in fe and k in wr))
         res["traffic_by_kernel"] = {k: int(2 * _med(fe[k].get("FETCH_SIZE")) * 1024 +
                                            _med(wr.get(k, {}).get("WRITE_SIZE")) * 1024) for k in fe}
     if va and kernel in va:

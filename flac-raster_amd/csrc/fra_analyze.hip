@@ -22,6 +22,7 @@
 //      sums, Rice estimate per partition leader, per-order totals by DPP wave sums
 //   6. winner = first minimal estimate (DPP argmin); exact Rice bits for the winner with k refined
 //      over k-1..k+1; VERBATIM if not smaller
+#include <algorithm>
 #include <type_traits>
 
 #if defined(FRA_STAMPS) && defined(FRA_STAMPS_FINE)
@@ -516,45 +517,26 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 // workgroup, r03 v12).  A hint only: nothing depends on it but the speed.  0 = off.
 #define FRA_PREFETCH 1024
 #endif
-template <typename T, int DIST>
-__device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {
-  const uint32_t nx = gridDim.x;
-  const uint64_t L = (uint64_t)blockIdx.x + (uint64_t)blockIdx.y * nx + DIST;
-  if (L >= (uint64_t)nx * gridDim.y) return 0u;
-  const int xp = (int)(L % nx), yp = (int)(L / nx);  // uniform
-  const FrameDev f2 = a.frames[a.frame_base + xp];
-  const StreamDev s2 = a.streams[f2.stream];
-  if (yp >= s2.channels || s2.ms || f2.n != kMaxBlock || s2.col_stride != 1) return 0u;
-  const char* b0 = (const char*)((const T*)a.raster + s2.base_off + (int64_t)yp * s2.band_stride +
-                                 (int64_t)f2.row0 * s2.row_stride);
-  const uint32_t w = (uint32_t)s2.width, rsb = (uint32_t)s2.row_stride * (uint32_t)sizeof(T);
-  // the 64-sample run of this lane (inside the subframe: n == 4096) spans <= 128 bytes: its first and
-  // last samples cover every line it touches (dword-aligned down)
-  auto word = [&](uint32_t c) -> uint32_t {
-    const uint32_t q = c / w;
-    return *(const uint32_t*)(b0 + ((q * rsb + (c - q * w) * (uint32_t)sizeof(T)) & ~3u));
-  };
-  const uint32_t c0 = (uint32_t)f2.col0 + 64u * (uint32_t)lane;
-  return word(c0) ^ word(c0 + 63u);
-}
 
+// One subframe by one workgroup: frame g, grid row cy (the channel, or for the 32-bit instance of a mid-side
+// stream the virtual channel cy + 2); rot rotates the wave roles; pf_allowed: the L2 prefetch may guess the
+// next workgroups by dispatch order (not in the redo-list mode)
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
+__device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, const int g, const int cy, const int rot,
+                                           const bool pf_allowed, AnalyzeSmem<B32, MAXLAG>& S) {
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
-  __shared__ AnalyzeSmem<B32, MAXLAG> S;
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
   // 7-wave 16-bit instance
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int g = a.flist ? a.flist[blockIdx.x] : a.frame_base + (int)blockIdx.x;
   // role of this wave (Levinson-Durbin, model searches, descriptor writes): rotated per workgroup so the
   // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
   // the encoder's scan) keeps the physical wave index wv
-  const int rw = (wv + (int)((blockIdx.x + blockIdx.y) & 3)) & 3;
+  const int rw = (wv + rot) & 3;
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
   // 16-bit instance, M and S (bps + 1 bits) by the 32-bit one, whose grid rows 0-1 are channels 2-3
-  const int c = (int)blockIdx.y + ((B32 && st.ms) ? 2 : 0);
+  const int c = cy + ((B32 && st.ms) ? 2 : 0);
   FRA_STAMP(0)
   if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
   const int n = fr.n;
@@ -587,7 +569,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
     if constexpr (!B32) {
       if (lut && a.vec8 && a.off32 && n == kMaxBlock) {
         done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
-        pf_ok = done && !a.flist;  // (the prefetch target is found by dispatch order)
+        pf_ok = done && pf_allowed;  // (the prefetch target is found by dispatch order)
       }
     }
     if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
@@ -1482,6 +1464,24 @@ read_x28(S.smp, t, x);
   }
 }
 
+template <bool B32, int MAXLAG>
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
+  __shared__ AnalyzeSmem<B32, MAXLAG> S;
+  if (a.redo) {
+    // redo-list mode (after k_analyze_w): the subframes it handed back, entry = frame * 8 + channel, by a
+    // grid of workgroups striding over the list
+    const int cnt = (int)__builtin_amdgcn_readfirstlane((int)*a.redo_count);
+    for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
+      __syncthreads();  // the previous entry's LDS is dead
+      const int e = __builtin_amdgcn_readfirstlane(a.redo[i]);
+      analyze_wg<B32, MAXLAG>(a, src, e >> 3, e & 7, i & 3, false, S);
+    }
+    return;
+  }
+  analyze_wg<B32, MAXLAG>(a, src, a.frame_base + (int)blockIdx.x, (int)blockIdx.y, (int)((blockIdx.x + blockIdx.y) & 3),
+                          true, S);
+}
+
 #ifdef FRA_STAMPS
 }  // namespace fra
 extern "C" __attribute__((visibility("default"))) int fra_diag_stamps(void* host, unsigned long long bytes) {
@@ -1498,29 +1498,29 @@ namespace fra {
 
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s);
 
-// slow != null (16-bit plans whose full frames k_analyze_w takes, fra_api.hip wave_path): k_analyze_w over
-// the launch's frames, then k_analyze over the nslow partial frames slow[0..nslow) of the launch's range
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, const int32_t* slow,
-                          int nslow) {
+// wave: 16-bit plans whose full frames k_analyze_w takes (fra_api.hip wave_path): k_analyze_w over the launch's
+// frames, handing partial frames and the subframes it does not finish (winner not its kept LPC model, VERBATIM,
+// an encode that would overrun its samples) to a redo list that k_analyze then works through; redo / redo_count
+// are the list and its counter (zeroed here first), capacity frames x channels
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, int32_t* redo,
+                          unsigned* redo_count, int max_redo_blocks) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-  if (slow && !b32) {
-    hipError_t e = launch_analyze_w(src, a.level, a, ms ? 2 : a.cmax, s);
+  if (wave && !b32 && ml == 8) {
+    const int cw = ms ? 2 : a.cmax;
+    hipError_t e = hipMemsetAsync(redo_count, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    if (nslow > 0) {
-      JobArgs sa = a;
-      sa.flist = slow;
-      sa.frame_count = nslow;
-      dim3 sg((unsigned)nslow, (unsigned)(ms ? 2 : a.cmax));
-      if (ml == 0) k_analyze<false, 0><<<sg, kThreads, 0, s>>>(sa, src);
-      else k_analyze<false, 8><<<sg, kThreads, 0, s>>>(sa, src);
-    }
+    JobArgs wa = a;
+    wa.redo = redo;
+    wa.redo_count = redo_count;
+    if ((e = launch_analyze_w(src, a.level, wa, cw, s)) != hipSuccess) return e;
+    const int cap = a.frame_count * cw;
+    k_analyze<false, 8><<<(unsigned)std::min(cap, max_redo_blocks), kThreads, 0, s>>>(wa, src);
     if (ms) {
       grid.y = 2;
-      if (ml == 0) k_analyze<true, 0><<<grid, kThreads, 0, s>>>(a, src);
-      else k_analyze<true, 8><<<grid, kThreads, 0, s>>>(a, src);
+      k_analyze<true, 8><<<grid, kThreads, 0, s>>>(a, src);
     }
     return hipGetLastError();
   }

@@ -26,6 +26,8 @@
 // and a spare one behind (look-ahead of the last chunk, multiplied by zero window coefficients); the
 // encoded subframe's bit buffer aliases the samples once the winner's residuals are in registers; a
 // 1.25 KiB scratch holds partition sums and the partition-search nodes.
+#include <type_traits>
+
 #include "fra_device.h"
 
 namespace fra {
@@ -38,6 +40,7 @@ constexpr int kWIters = kWChunks / 64;        // chunks per lane
 struct WaveSmem {
   uint32_t sw[8 + 8 * (kWChunks + 1) + 2 * (kWChunks / 8)];  // zero chunk, 256 chunks (+ pads), spare chunk
   unsigned long long scr[160];          // FIXED partition sums (u32 [5][64]) / LPC sums / search nodes
+  int32_t mdl[3][12];                   // LPC model of window wi: q[0..7], shift, order, ok
 };
 // the bit buffer: <= 2,049 words (exact < verbatim = 8 + 65,536 bits) + one spare zeroed word
 static_assert(sizeof(WaveSmem::sw) >= 4 * 2050, "bit buffer inside the sample array");
@@ -47,23 +50,31 @@ __device__ __forceinline__ int32_t wsample(const uint32_t* sw, int s) {
   const uint32_t v = sw[sdw(s >> 4, (s & 15) >> 1)];
   return (s & 1) ? hi16(v) : lo16(v);
 }
-__device__ __forceinline__ void wsync() {  // this wave's LDS stores -> its own reads
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+// this wave's LDS stores -> its own reads (and reads before later stores): the DS instructions of one wave
+// execute in order, so only the compiler must not move LDS accesses across this point -- no s_waitcnt
+__device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 // D[0..5] = the last 12 samples of chunk t - 1, D[6..13] = chunk t (int16 pairs, sample 16t - 12 + 2k in
 // the low half of D[k]) -- the layout read_d14 gives k_analyze
-__device__ __forceinline__ void wread_d14(const uint32_t* sw, int t, uint32_t (&D)[14]) {
+// Chunk t = 64 j + lane starts at dword own(lane) + 528 j (528 = 64 chunks of 8 + 8 pads); its predecessor
+// at prev(lane) + 528 j, its successor at next(lane) + 528 j.  Every sample read is one of these three
+// per-lane bases + 528 j + an immediate offset (no per-access address registers)
+constexpr int kWIterDw = 8 * 64 + 2 * 8;
+__device__ __forceinline__ int base_own(int lane) { return 8 + 8 * lane + 2 * (lane >> 3); }
+__device__ __forceinline__ int base_prev(int lane) { return 8 * lane + 2 * ((lane - 1) >> 3); }
+__device__ __forceinline__ int base_next(int lane) { return 16 + 8 * lane + 2 * ((lane + 1) >> 3); }
+__device__ __forceinline__ void wread_d14(const uint32_t* po, const uint32_t* pp, uint32_t (&D)[14]) {
 #pragma unroll
   for (int p = 0; p < 3; p++) {
-    const uint2 v = *reinterpret_cast<const uint2*>(&sw[sdw(t - 1, 2 + 2 * p)]);
+    const uint2 v = *reinterpret_cast<const uint2*>(pp + 2 + 2 * p);
     D[2 * p] = v.x;
     D[2 * p + 1] = v.y;
   }
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const uint2 v = *reinterpret_cast<const uint2*>(&sw[sdw(t, 2 * p)]);
+    const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
     D[6 + 2 * p] = v.x;
     D[7 + 2 * p] = v.y;
   }
@@ -144,14 +155,16 @@ __host__ __device__ constexpr int lag_slot(int lag) {  // (k << 2) | r of the fi
   return -1;
 }
 
-// Levinson-Durbin (op sequence of levinson_wave / oracle ora_levinson) where each lane also keeps the
-// coefficient row of ITS order lo (row of order lo = lpc after step lo - 1), so the rows need no LDS
+// Levinson-Durbin (op sequence of levinson_wave / oracle ora_levinson) where each lane keeps only what its
+// order lo needs: the prediction error after step lo - 1 (e, step 0's for lo = 0) and that step's row,
+// negated (lp = -lpc, the quantiser's input), so neither the rows nor the errors go through LDS
 template <int MAXLAG>
-__device__ inline int levinson_keep(const double (&ac)[MAXLAG + 1], int max_order, double (&errv)[MAXLAG],
-                                    double (&row)[MAXLAG], int lo) {
+__device__ inline int levinson_keep(const double (&ac)[MAXLAG + 1], int max_order, double& e, double (&lp)[MAXLAG],
+                                    int lo) {
   double lpc[MAXLAG];
 #pragma unroll
-  for (int j = 0; j < MAXLAG; j++) { lpc[j] = 0.0; errv[j] = 0.0; row[j] = 0.0; }
+  for (int j = 0; j < MAXLAG; j++) { lpc[j] = 0.0; lp[j] = 0.0; }
+  e = 0.0;
   double err = ac[0];
   int result = max_order;
   bool done = false;
@@ -173,8 +186,8 @@ __device__ inline int levinson_keep(const double (&ac)[MAXLAG + 1], int max_orde
       err = err * (1.0 - r * r);
       const bool mine = lo == i + 1;
 #pragma unroll
-      for (int j = 0; j <= i; j++) row[j] = mine ? lpc[j] : row[j];
-      errv[i] = err;
+      for (int j = 0; j <= i; j++) lp[j] = mine ? -lpc[j] : lp[j];
+      e = (mine || (i == 0 && lo == 0)) ? err : e;
       if (!(err > 0.0)) {
         result = (err == 0.0) ? i + 1 : i;
         done = true;
@@ -378,7 +391,8 @@ __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st,
   vmax = max(vmax, max((int32_t)pmax.x, (int32_t)pmax.y));
 }
 
-// 16-bit path: sum of |LPC residual| of order O over one chunk (lpc_abs16_raw without the kept residuals)
+// 16-bit path: sum of |LPC residual| of order O over one chunk (lpc_abs16_raw without the kept residuals),
+// warm-up positions (< O, chunk 0) masked
 template <int O>
 __device__ __forceinline__ uint32_t lpc_abs16_w(const uint32_t (&D)[14], const int32_t* q, int sh, bool head) {
   constexpr int NP = (O + 1) / 2;
@@ -394,20 +408,78 @@ __device__ __forceinline__ uint32_t lpc_abs16_w(const uint32_t (&D)[14], const i
   return acc;
 }
 
+// the same sum, plus the chunk's zig-zag residuals packed two per dword (u[2p] low, u[2p+1] high; exact
+// whenever every u < 2^16, which `um`, the OR of all u, tells)
+template <int O>
+__device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const int32_t* q, int sh, bool head,
+                                                 uint32_t (&pk)[kChunk / 2], uint32_t& um) {
+  constexpr int NP = (O + 1) / 2;
+  fra_short2 Q[NP];
+  q_pairs_rev<NP>(q, Q);
+  uint32_t acc = 0;
+  uint32_t u[kChunk];
+#pragma unroll
+  for (int jj = 0; jj < kChunk; jj++) {
+    const int32_t r = sample_at(D, 12 + jj) - (pred_raw<NP>(D, 12 + jj, Q) >> sh);
+    const uint32_t rb = (uint32_t)r ^ kBias;
+    const bool warm = jj < O && head;
+    acc = sad_acc(rb, warm ? rb : kBias, acc);
+    u[jj] = warm ? 0u : zz32(r);
+    um |= u[jj];
+  }
+#pragma unroll
+  for (int p = 0; p < kChunk / 2; p++) pk[p] = (u[2 * p + 1] << 16) | (u[2 * p] & 0xFFFFu);
+  return acc;
+}
+
 }  // namespace
+
+#ifdef FRA_STAMPS
+// diagnostic build only (csrc/Makefile `wstamps`, tools/wstamp_phases.py): lane 0 of the first kWStampW waves
+// stores s_memtime after each phase, inside the real steady state
+constexpr unsigned kWStampW = 1u << 18, kWStampN = 10;
+__device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
+#define FRA_WSTAMP(k)                                                                            \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = __builtin_amdgcn_s_memtime();      \
+  }
+#define FRA_WSTAMP_VAL(k, v)                                                                     \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = (unsigned long long)(v);            \
+  }
+#else
+#define FRA_WSTAMP(k)
+#define FRA_WSTAMP_VAL(k, v)
+#endif
+
+// prefetch distance in waves: ~a quarter of the 4,096 waves resident chip-wide (16 per CU), so the rows are
+// in L2 (1 MiB of rows per XCD in flight) when that wave starts
+constexpr int kWPrefetch = 1024;
 
 template <int MAXLAG>
 __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
-  static_assert(MAXLAG == 0 || MAXLAG == 8, "levels 0-6");
+  static_assert(MAXLAG == 8, "levels 3-6");
   __shared__ WaveSmem S;
   uint32_t* const sw = S.sw;
   const int lane = (int)threadIdx.x;
+  FRA_WSTAMP(0)
+  const int bo = base_own(lane), bpv = base_prev(lane), bnx = base_next(lane);
   const int g = a.frame_base + (int)blockIdx.x;
   const int c = (int)blockIdx.y;
   const FrameDev fr = a.frames[g];
-  if (fr.n != kMaxBlock) return;  // partial frames: k_analyze over the frame list
   const StreamDev st = a.streams[fr.stream];
   if (c >= (st.ms ? 2 : st.channels)) return;
+  // a subframe this kernel does not finish: appended to the redo list that k_analyze works through next
+  auto hand_back = [&](int why) {
+    FRA_WSTAMP_VAL(9, why)
+    if (lane == 0) a.redo[atomicAdd(a.redo_count, 1u)] = g * 8 + c;
+  };
+  if (fr.n != kMaxBlock) {  // partial last frames
+    hand_back(1);
+    return;
+  }
   constexpr int n = kMaxBlock;
   const int bps = st.bps;
   const LevelCfg cfg = level_cfg(a.level);
@@ -417,17 +489,19 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   // ---- 1. load + normalise (table gather), OR / min / max
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-  {
+  auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx) {
     const int32_t* lut = a.lut + (int64_t)fr.stream * a.lut_stride;
     if (lane < 8) sw[lane] = 0u;  // zero chunk
     switch (src) {  // wave-uniform
-      case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, orv, vmin, vmax); break;
-      case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, orv, vmin, vmax); break;
-      case ST_U16: wload_lut<ST_U16>(a.raster, st, fr, c, lut, sw, lane, orv, vmin, vmax); break;
-      default: wload_lut<ST_I16>(a.raster, st, fr, c, lut, sw, lane, orv, vmin, vmax); break;
+      case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
+      case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
+      case ST_U16: wload_lut<ST_U16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
+      default: wload_lut<ST_I16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
     }
-  }
+  };
+  load_samples(orv, vmin, vmax);
   orv = wave_or32(orv);
+  FRA_WSTAMP(1)
   vmin = (int32_t)(wave_min32((uint32_t)vmin ^ 0x80000000u) ^ 0x80000000u);
   vmax = (int32_t)(~wave_min32(~((uint32_t)vmax ^ 0x80000000u)) ^ 0x80000000u);
 
@@ -445,14 +519,19 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   }
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
-  if (w) {  // samples >>= w (int16 pairs, arithmetic; the pad dwords too)
+  auto shift_wasted = [&]() {  // samples >>= w (int16 pairs, arithmetic; the pad dwords too)
     for (int k = lane; k < sdw(kWChunks, 0) - 8; k += 64) {
       const uint32_t v = sw[8 + k];
       const uint32_t lo = (uint32_t)(lo16(v) >> w) & 0xFFFFu, hi = (uint32_t)(hi16(v) >> w);
       sw[8 + k] = lo | (hi << 16);
     }
-  }
+  };
+  if (w) shift_wasted();
   wsync();
+  // L2 prefetch of the rows of the subframe kWPrefetch waves ahead (issued after this wave's own loads and
+  // gathers: nothing waits for it until the window coefficient loads, long after it landed)
+  const uint32_t pf = (src == ST_U16 || src == ST_I16) ? prefetch_rows<uint16_t, kWPrefetch>(a, lane)
+                                                       : prefetch_rows<uint8_t, kWPrefetch>(a, lane);
   const uint32_t hdr = 8u + (uint32_t)w;
   const uint32_t verb = hdr + (uint32_t)n * (uint32_t)sbps;
   const int P = max_porder(n, 0, cfg.max_porder);  // = cfg.max_porder (3..6)
@@ -466,7 +545,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
     const int t = 64 * j + lane;
     const bool head = t == 0;
     uint32_t D[14];
-    wread_d14(sw, t, D);
+    wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
     int32_t x[28];
     unpack28(D, x);
 #pragma unroll
@@ -492,6 +571,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
 #pragma unroll
   for (int k = 0; k < 5; k++) pfix[k] = lane < (1 << P) ? scr32[k * 64 + lane] : 0u;
   wsync();
+  FRA_WSTAMP(2)
 
   // ---- running winner (FRA-1 3.8: first minimal estimate in model order)
   uint32_t west = 0xFFFFFFFFu;
@@ -506,29 +586,36 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
     }
   };
 
-  // ---- 5a. FIXED candidates (3.7) and their partition search
-  {
-    int g1, g2;
-    fixed_guess2_w(pfix, P, lane, g1, g2);
+  // ---- 5a. FIXED candidates (3.7): the two orders with the smallest totals; their partition sums stay
+  // in registers for the candidate loop below
+  int g1, g2;
+  fixed_guess2_w(pfix, P, lane, g1, g2);
+  uint32_t pf1 = 0, pf2 = 0;
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-      const int m = r == 0 ? g1 : g2;
-      if (m < 0) continue;
-      uint32_t pm_sum = 0;
-#pragma unroll
-      for (int k = 0; k < 5; k++) pm_sum = k == m ? pfix[k] : pm_sum;
-      const int pm = max_porder(n, m, cfg.max_porder);
-      uint64_t best;
-      int bp;
-      uint32_t kreg;
-      porder_search_w(pm_sum, S.scr, P, pm, n, m, lane, best, bp, kreg);
-      offer((uint32_t)(hdr + (uint64_t)m * sbps + best), m, 2, m, 0, nullptr, bp, kreg);
-    }
+  for (int k = 0; k < 5; k++) {
+    pf1 = k == g1 ? pfix[k] : pf1;
+    pf2 = k == g2 ? pfix[k] : pf2;
   }
-
-  // ---- 3. LPC analysis per apodization window (3.4-3.7)
+#if defined(FRA_WPAD) && FRA_WPAD > 0
+  {  // diagnostic build only (tools/gpu_r04_pad.sh): FRA_WPAD extra independent VALU instructions per wave
+    uint32_t p0 = lane, p1 = lane + 1, p2 = lane + 2, p3 = lane + 3;
+#pragma unroll
+    for (int k = 0; k < FRA_WPAD / 4; k++) {
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p0) : "v"(p1));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p1) : "v"(p2));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p2) : "v"(p3));
+      asm volatile("v_add_u32 %0, %0, %1" : "+v"(p3) : "v"(p0));
+    }
+    if ((p0 ^ p1 ^ p2 ^ p3) == 0x7FFFFFF3u) S.mdl[0][11] = 1;  // keep the chains alive
+  }
+#endif
+  FRA_WSTAMP(3)
+  // ---- 3. LPC analysis per apodization window (3.4-3.7): lane 16 wi + o_l of window wi's lane group holds
+  // that window's model (order o_l, quantised q, shift qsh, ok)
+  int nlpc = 0;
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
+      nlpc = a.nwin;
       const int nwin = a.nwin;
       constexpr int NL = MAXLAG + 1, N16 = ((NL + 1) / 2 + 1) / 2;
       double acl[NL];
@@ -548,29 +635,34 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           // every chunk partial is +0.0 (k_analyze's inactive wave)
           if (lo < 1024 * j + 1024 + MAXLAG && hi > 1024 * j) {
             const int t = 64 * j + lane, i0 = kChunk * t;
-            // coefficients: exactly 1.0f inside the plateau (the product is the sample itself); else
-            // loaded, entries at or past n are 0.0f (load_window)
-            float wc[kChunk + MAXLAG];
-            const bool plat = i0 >= plo && i0 + kChunk + MAXLAG <= phi;
-            if (plat) {
-#pragma unroll
-              for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = 1.0f;
-            } else {
-              load_window<MAXLAG>(win, i0, n, wc);
-            }
             int32_t y[kChunk + MAXLAG];  // samples 16t .. 16t + 15 + MAXLAG (dword pairs: ds_read_b64)
 #pragma unroll
             for (int p = 0; p < (kChunk + MAXLAG) / 4; p++) {
-              const int tt = p < kChunk / 4 ? t : t + 1, dd = 2 * (p % (kChunk / 4));
-              const uint2 v = *reinterpret_cast<const uint2*>(&sw[sdw(tt, dd)]);
+              const uint32_t* src = sw + (p < kChunk / 4 ? bo : bnx) + kWIterDw * j + 2 * (p % (kChunk / 4));
+              const uint2 v = *reinterpret_cast<const uint2*>(src);
               y[4 * p] = lo16(v.x);
               y[4 * p + 1] = hi16(v.x);
               y[4 * p + 2] = lo16(v.y);
               y[4 * p + 3] = hi16(v.y);
             }
+            // coefficients exactly 1.0f inside the plateau: the product is the sample itself (no load, and
+            // no multiply when the whole iteration lies inside); else loaded, entries at or past n 0.0f
+            const bool plat = i0 >= plo && i0 + kChunk + MAXLAG <= phi;
             float wf[kChunk + MAXLAG];
+            if (__all(plat)) {
 #pragma unroll
-            for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = plat ? (float)y[jx] : (float)y[jx] * wc[jx];
+              for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = (float)y[jx];
+            } else {
+              float wc[kChunk + MAXLAG];
+              if (plat) {
+#pragma unroll
+                for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = 1.0f;
+              } else {
+                load_window<MAXLAG>(win, i0, n, wc);
+              }
+#pragma unroll
+              for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = (float)y[jx] * wc[jx];
+            }
             f32x2 pacc[NL];
 #pragma unroll
             for (int l = 0; l < NL; l++) pacc[l] = f32x2{0.0f, 0.0f};
@@ -607,17 +699,14 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           acl[l] = gw == wi ? tot : acl[l];
         }
       }
+      FRA_WSTAMP(4)
       // Levinson-Durbin, order choice and quantisation of up to 4 windows at once: window wi on lanes
       // 16 wi .. +15 (the same op sequence per lane); lane 16 wi + o holds order o's row and quantisation
       const int gw = lane >> 4, lo = lane & 15;
       const bool gon = gw < nwin;
-      double row[MAXLAG], errv[MAXLAG];
+      double lpo[MAXLAG], e = 0.0;
       int nord = 0;
-      if (gon && acl[0] != 0.0) nord = levinson_keep<MAXLAG>(acl, lmax, errv, row, lo);
-      double e = errv[0];
-#pragma unroll
-      for (int jx = 1; jx < MAXLAG; jx++)
-        if (lo == jx + 1) e = errv[jx];
+      if (gon && acl[0] != 0.0) nord = levinson_keep<MAXLAG>(acl, lmax, e, lpo, lo);
       const bool on = nord > 0 && lo >= 1 && lo <= nord;
       const uint64_t key = on ? (uint64_t)__double_as_longlong(order_bits(e, n, lo, prec + sbps)) : ~0ull;
       uint64_t rk = min(key, dpp64_old<DPP_SHR1, 0xF>(key, ~0ull));
@@ -628,33 +717,93 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       const uint64_t bal = __ballot(on && key == kmin);
       const uint32_t rowbits = (uint32_t)(bal >> (16 * gw)) & 0xFFFFu;
       // every lane quantises its own order's row; the window's model is lane 16 wi + o
-      bool ok = false;
-      int qsh = 0;
       int32_t q[MAXLAG];
 #pragma unroll
       for (int jx = 0; jx < MAXLAG; jx++) q[jx] = 0;
-      {
-        double lpo[MAXLAG];
-#pragma unroll
-        for (int jx = 0; jx < MAXLAG; jx++) lpo[jx] = jx < lo ? -row[jx] : 0.0;  // lp = -lpc
-        if (on) ok = quantize<MAXLAG>(lpo, lo, prec, q, qsh);
-      }
+      bool ok = false;
+      int qsh = 0;
+      if (on) ok = quantize<MAXLAG>(lpo, lo, prec, q, qsh);
       const int o_l = nord > 0 ? (int)__builtin_ctz(rowbits | 0x10000u) : 0;
-      // ---- 4+5. per window: residual sums of the model at the finest partitions, partition search
-      for (int wi = 0; wi < nwin; wi++) {
-        const int o = __builtin_amdgcn_readlane(o_l, 16 * wi);
-        if (o == 0) continue;  // LD found no order (nord 0)
-        const int L = 16 * wi + o;
-        if (!__builtin_amdgcn_readlane((int)ok, L)) continue;
-        const int sh = __builtin_amdgcn_readlane(qsh, L);
-        int32_t qm[8];
+      if (gon && lo == o_l) {  // the window's model (o_l = 0: none) to LDS for the candidate loop
 #pragma unroll
-        for (int jx = 0; jx < 8; jx++) qm[jx] = jx < MAXLAG ? __builtin_amdgcn_readlane(q[jx < MAXLAG ? jx : 0], L) : 0;
+        for (int jx = 0; jx < 8; jx++) S.mdl[gw][jx] = jx < MAXLAG ? q[jx < MAXLAG ? jx : 0] : 0;
+        S.mdl[gw][8] = qsh;
+        S.mdl[gw][9] = o_l;
+        S.mdl[gw][10] = ok ? 1 : 0;
+      }
+      wsync();
+    }
+  }
+  FRA_WSTAMP(5)
+
+  // ---- 4+5. the candidates in model order -- FIXED g1, g2, then each window's LPC model -- one partition
+  // search each (one code body); an LPC model first gets its residual sums at the finest partitions.
+  // The last window with a model is summed last: its pass replaces each chunk's samples in LDS by the
+  // chunk's zig-zag residuals (int16 pairs), which the exact pass and the encoder then read instead of
+  // recomputing the predictor twice (fallback: the samples are loaded again)
+  int keep_wi = -1;
+  for (int wi = 0; wi < nlpc; wi++)
+    if (S.mdl[wi][9] != 0 && S.mdl[wi][10] != 0) keep_wi = wi;
+  keep_wi = __builtin_amdgcn_readfirstlane(keep_wi);
+  bool kept_fit = false;
+  uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
+#pragma unroll 1
+  for (int ci = 0; ci < 2 + nlpc; ci++) {
+    int m, o, sh = 0, type = 2;
+    int32_t qm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t psum;
+    if (ci < 2) {
+      m = o = ci == 0 ? g1 : g2;
+      psum = ci == 0 ? pf1 : pf2;
+    } else {
+      const int wi = ci - 2;
+      o = __builtin_amdgcn_readfirstlane(S.mdl[wi][9]);
+      if (o == 0 || !__builtin_amdgcn_readfirstlane(S.mdl[wi][10])) continue;  // no order / not quantisable
+      m = 5 + wi;
+      type = 3;
+      sh = __builtin_amdgcn_readfirstlane(S.mdl[wi][8]);
+#pragma unroll
+      for (int jx = 0; jx < 8; jx++) qm[jx] = __builtin_amdgcn_readfirstlane(S.mdl[wi][jx]);
+      if (wi == keep_wi) {
+        uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+        for (int j = 0; j < kWIters; j++) {
+          const int t = 64 * j + lane;
+          const bool head = t == 0;
+          uint32_t* const po = sw + bo + kWIterDw * j;
+          uint32_t D[14];
+          wread_d14(po, sw + bpv + kWIterDw * j, D);
+          if (j > 0) {  // chunk 64 j - 1 already holds residuals: its last 12 samples came from lane 63
+#pragma unroll
+            for (int k = 0; k < 6; k++) D[k] = lane == 0 ? carry[k] : D[k];
+          }
+#pragma unroll
+          for (int k = 0; k < 6; k++) carry[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[8 + k], 63);
+          if (j == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) w4[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[6 + k], 0);
+          }
+          uint32_t acc = 0, pk[kChunk / 2];
+          switch (o) {
+#define FRA_CASE(O_) \
+  case O_: acc = lpc_abs16_pk<O_>(D, qm, sh, head, pk, um); break;
+            FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6) FRA_CASE(7) FRA_CASE(8)
+#undef FRA_CASE
+          }
+          wsync();  // (all lanes' sample reads of this iteration precede the stores)
+#pragma unroll
+          for (int p = 0; p < kChunk / 4; p++) *reinterpret_cast<uint2*>(po + 2 * p) = make_uint2(pk[2 * p], pk[2 * p + 1]);
+          const uint64_t gs = group_sum_auto(2ull * acc, gsl);
+          if ((lane & ((1 << gsl) - 1)) == (1 << gsl) - 1) S.scr[t >> gsl] = gs;
+        }
+        kept_fit = !__any(um > 0xFFFFu);
+      } else {
+#pragma unroll 1
         for (int j = 0; j < kWIters; j++) {
           const int t = 64 * j + lane;
           const bool head = t == 0;
           uint32_t D[14];
-          wread_d14(sw, t, D);
+          wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
           uint32_t acc = 0;
           switch (o) {
 #define FRA_CASE(O_) \
@@ -665,71 +814,119 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           const uint64_t gs = group_sum_auto(2ull * acc, gsl);
           if ((lane & ((1 << gsl) - 1)) == (1 << gsl) - 1) S.scr[t >> gsl] = gs;
         }
-        wsync();
-        const uint64_t ps = lane < (1 << P) ? S.scr[lane] : 0ull;
-        wsync();
-        const int pm = max_porder(n, o, cfg.max_porder);
-        uint64_t best;
-        int bp;
-        uint32_t kreg;
-        porder_search_w(ps, S.scr, P, pm, n, o, lane, best, bp, kreg);
-        offer((uint32_t)(hdr + (uint64_t)o * sbps + 9 + (uint64_t)o * prec + best), 5 + wi, 3, o, sh, qm, bp, kreg);
       }
+      wsync();
+      psum = lane < (1 << P) ? S.scr[lane] : 0ull;
+      wsync();
     }
+    const int pm = max_porder(n, o, cfg.max_porder);
+    uint64_t best;
+    int bp;
+    uint32_t kreg;
+    porder_search_w(psum, S.scr, P, pm, n, o, lane, best, bp, kreg);
+    const uint64_t est = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + best;
+    offer((uint32_t)est, m, type, o, sh, qm, bp, kreg);
   }
 
-  // ---- 6. the winner's residuals (zig-zag, warm-up samples 0), exact Rice bits with k refined (3.9)
+  FRA_WSTAMP(6)
+  // ---- 6. the winner's zig-zag residuals in LDS, int16 pairs in the samples' place: the kept ones, or (any
+  // other winner: a FIXED order, another window) the samples loaded again if the keep pass overwrote them
+  // and the winner's residuals written the same way.  Residuals past 16 bits, VERBATIM or an encode that would
+  // overrun its residuals in the aliased bit buffer: the subframe goes to k_analyze
   const int type = wtype, o = wo, sh = wsh, ps = wps;
+  if (!(type == 3 && wm == 5 + keep_wi && kept_fit)) {
+    if (type == 3 && wm == 5 + keep_wi) {  // the kept model, but some residual needs more than 16 bits
+      hand_back(5);
+      return;
+    }
+    if (keep_wi >= 0) {
+      wsync();
+      uint32_t ov = 0;
+      int32_t mn = 0, mx = 0;
+      load_samples(ov, mn, mx);
+      if (w) shift_wasted();
+      wsync();
+    }
+    fra_short2 Q[4];
+    q_pairs_rev<4>(wq, Q);
+    uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+    for (int j = 0; j < kWIters; j++) {
+      const int t = 64 * j + lane;
+      uint32_t* const po = sw + bo + kWIterDw * j;
+      uint32_t D[14];
+      wread_d14(po, sw + bpv + kWIterDw * j, D);
+      if (j > 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) D[k] = lane == 0 ? carry[k] : D[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) carry[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[8 + k], 63);
+      if (j == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) w4[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[6 + k], 0);
+      }
+      uint32_t u[kChunk];
+      if (type == 3) {
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) u[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
+      } else {  // FIXED: the o-th finite difference
+        int32_t x[28];
+        unpack28(D, x);
+#pragma unroll
+        for (int k = 1; k <= 4; k++) {
+          if (k <= o) {
+#pragma unroll
+            for (int jx = 12 + kChunk - 1; jx >= 8 + k; jx--) x[jx] = x[jx] - x[jx - 1];
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) u[jj] = zz32(x[12 + jj]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 12; jj++)
+        if (t == 0 && jj < o) u[jj] = 0u;
+#pragma unroll
+      for (int jj = 0; jj < kChunk; jj++) um |= u[jj];
+      wsync();
+#pragma unroll
+      for (int p = 0; p < kChunk / 4; p++)
+        *reinterpret_cast<uint2*>(po + 2 * p) = make_uint2((u[4 * p + 1] << 16) | (u[4 * p] & 0xFFFFu),
+                                                           (u[4 * p + 3] << 16) | (u[4 * p + 2] & 0xFFFFu));
+    }
+    if (__any(um > 0xFFFFu)) {
+      hand_back(type == 3 ? 4 : 3);
+      return;
+    }
+  }
   const int pz = n >> ps;
   const int tl = 8 - ps;                  // log2 chunks per partition (2..8)
   const int ls = tl < 6 ? tl : 6;         // lanes per partition group inside one iteration
   const int npp = 1 << ps;
-  int32_t warm = 0;
-  if (lane < o) warm = wsample(sw, lane);
-  fra_short2 Q[4];
-  q_pairs_rev<4>(wq, Q);
-  // zig-zag residuals of the winner for chunk 64 j + lane (warm-up positions 0)
+  int32_t warm;                           // warm-up sample `lane` (saved by the keep pass)
+  {
+    const uint32_t wv2 = lane >= 6 ? w4[3] : lane >= 4 ? w4[2] : lane >= 2 ? w4[1] : w4[0];
+    warm = lane < o ? ((lane & 1) ? hi16(wv2) : lo16(wv2)) : 0;
+  }
+  // the residuals of chunk 64 j + lane (warm-up positions 0): its 8 dwords of int16 pairs
   auto residuals = [&](int j, uint32_t (&un)[kChunk]) {
-    const int t = 64 * j + lane;
-    uint32_t D[14];
-    wread_d14(sw, t, D);
-    if (type == 3) {
+    const uint32_t* po = sw + bo + kWIterDw * j;
 #pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
-    } else {  // FIXED: the o-th finite difference in place
-      int32_t x[28];
-      unpack28(D, x);
-#pragma unroll
-      for (int k = 1; k <= 4; k++) {
-        if (k <= o) {
-#pragma unroll
-          for (int jx = 12 + kChunk - 1; jx >= 8 + k; jx--) x[jx] = x[jx] - x[jx - 1];
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(x[12 + jj]);
-    }
-    if (t == 0) {
-#pragma unroll
-      for (int jj = 0; jj < 12; jj++)
-        if (jj < o) un[jj] = 0u;
+    for (int p = 0; p < kChunk / 4; p++) {
+      const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
+      un[4 * p] = v.x & 0xFFFFu;
+      un[4 * p + 1] = v.x >> 16;
+      un[4 * p + 2] = v.y & 0xFFFFu;
+      un[4 * p + 3] = v.y >> 16;
     }
   };
-  // per iteration (runtime j, explicit selects: no dynamically indexed registers)
-  auto sel4 = [](const uint32_t (&v)[kWIters], int j) -> uint32_t {
-    return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
-  };
-  auto set4 = [](uint32_t (&v)[kWIters], int j, uint32_t x) {
-#pragma unroll
-    for (int jx = 0; jx < kWIters; jx++) v[jx] = jx == j ? x : v[jx];
-  };
-  uint32_t kc[kWIters] = {0, 0, 0, 0};    // Rice parameter of the lane's chunk of iteration j
-  uint32_t fk[kWIters][3];                // sums of u >> (k0 - 1), u >> k0, u >> (k0 + 1) of that chunk
-  uint32_t k0r[kWIters] = {0, 0, 0, 0};
-  uint32_t bitsl = 0;                     // exact bits of the partitions this lane leads
+  uint32_t kc[kWIters];       // Rice parameter of the lane's chunk of iteration j
+  uint32_t fk[kWIters][3];    // sums of u >> (k0 - 1), u >> k0, u >> (k0 + 1) of that chunk (u < 2^16)
+  uint32_t k0r[kWIters];
+  uint32_t bitsl = 0;         // exact bits of the partitions this lane leads
   bool bigl = false;
-  uint64_t E[3] = {0, 0, 0};              // partitions spanning iterations (ps <= 1): running sums
-#pragma unroll 1
+  uint64_t E[3] = {0, 0, 0};  // partitions spanning iterations (ps <= 1): running sums
+#pragma unroll
   for (int j = 0; j < kWIters; j++) {
     const int t = 64 * j + lane;
     uint32_t un[kChunk];
@@ -737,31 +934,24 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
     const int pidx = t >> tl;
     const int k0 = __shfl((int)wk, pidx & 63, 64);
     const int km = k0 > 0 ? k0 - 1 : 0;
-    uint32_t f0 = 0, f1 = 0, f2 = 0;  // u < 2^28: 16 of them fit 32 bits
+    uint32_t f0 = 0, f1 = 0, f2 = 0;
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) {
       f0 += un[jj] >> km;
       f1 += un[jj] >> k0;
       f2 += un[jj] >> (k0 + 1);
     }
-#pragma unroll
-    for (int jx = 0; jx < kWIters; jx++) {
-      fk[jx][0] = jx == j ? f0 : fk[jx][0];
-      fk[jx][1] = jx == j ? f1 : fk[jx][1];
-      fk[jx][2] = jx == j ? f2 : fk[jx][2];
-    }
-    set4(k0r, j, (uint32_t)k0);
-    uint64_t v0, v1, v2;
-    if (__all(f0 <= (0xFFFFFFFFu >> ls))) {
-      v0 = group_sum32(f0, ls); v1 = group_sum32(f1, ls); v2 = group_sum32(f2, ls);
-    } else {
-      v0 = group_sum64(f0, ls); v1 = group_sum64(f1, ls); v2 = group_sum64(f2, ls);
-    }
+    fk[j][0] = f0;
+    fk[j][1] = f1;
+    fk[j][2] = f2;
+    k0r[j] = (uint32_t)k0;
+    // 16 u < 2^16 per lane: the group sums of <= 64 lanes fit 32 bits
+    const uint32_t v0 = group_sum32(f0, ls), v1 = group_sum32(f1, ls), v2 = group_sum32(f2, ls);
     if (tl <= 6) {  // the partition lies inside this iteration: its last lane decides
       int bk = 0;
       if ((lane & ((1 << ls) - 1)) == (1 << ls) - 1) {
         const uint64_t cnt = (uint64_t)(pz - (pidx == 0 ? o : 0));
-        const uint64_t ev[3] = {v0, v1, v2};
+        const uint32_t ev[3] = {v0, v1, v2};
         uint64_t best = 0;
         bool first = true;
 #pragma unroll
@@ -775,17 +965,14 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         bigl = bigl || bk > 14;
         d->k[pidx] = (uint8_t)bk;
       }
-      set4(kc, j, (uint32_t)__shfl(bk, lane | ((1 << ls) - 1), 64));
-    } else {  // ps <= 1: whole-iteration sums accumulate into the partition's running sums
-      auto rl64 = [](uint64_t v) -> uint64_t {
-        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63) |
-               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32);
-      };
-      E[0] += rl64(v0);
-      E[1] += rl64(v1);
-      E[2] += rl64(v2);
+      kc[j] = (uint32_t)__shfl(bk, lane | ((1 << ls) - 1), 64);
+    } else {  // ps <= 1: whole-iteration sums accumulate into the partition's running sums (uniform)
+      E[0] += (uint32_t)__builtin_amdgcn_readlane((int)v0, 63);
+      E[1] += (uint32_t)__builtin_amdgcn_readlane((int)v1, 63);
+      E[2] += (uint32_t)__builtin_amdgcn_readlane((int)v2, 63);
       const int span = 1 << (tl - 6);  // iterations per partition (2 or 4)
-      if (((j + 1) & (span - 1)) == 0) {  // partition complete: decide its parameter (uniform)
+      kc[j] = 0;
+      if (((j + 1) & (span - 1)) == 0) {  // partition complete: decide its parameter
         const int pq = j >> (tl - 6);
         const uint64_t cnt = (uint64_t)(pz - (pq == 0 ? o : 0));
         int bk = 0;
@@ -810,54 +997,16 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       }
     }
   }
+  FRA_WSTAMP(7)
   const bool big = __any(bigl);
   const uint64_t rtot = (uint64_t)wave_sum32(bitsl) + (uint64_t)npp * (big ? 5 : 4) + 6;
   const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
-  const bool verbatim = exact >= verb;
-  if (lane < kMaxLpc) {
-    int32_t cv = 0;
-#pragma unroll
-    for (int jq = 0; jq < 8; jq++) cv = lane == jq ? wq[jq] : cv;
-    d->coef[lane] = type == 3 ? cv : 0;
-  }
-  if (lane == 0) {
-    d->wasted = (uint8_t)w;
-    d->sbps = (uint8_t)sbps;
-    d->cval = 0;
-    if (verbatim) {
-      d->type = 1; d->order = 0; d->porder = 0; d->method = 0; d->precision = 0; d->shift = 0;
-      d->bits = verb;
-    } else {
-      d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
-      d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh;
-      d->bits = (uint32_t)exact;
-    }
-  }
-  const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
-  if (verbatim) {  // straight from the samples to the slot (the bit buffer is not touched)
-    const uint32_t nw = (verb + 31) >> 5;
-    for (uint32_t jw = lane; jw < nw; jw += 64) {
-      const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
-      const int64_t wb = 32 * (int64_t)jw;
-      uint32_t word = jw == 0 ? (uint32_t)(hv >> 32) : (jw == 1 ? (uint32_t)hv : 0u);
-      const int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
-      for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
-        const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
-        const int sft = 32 - (int)rel - sbps;
-        const uint64_t v = (uint64_t)((uint32_t)wsample(sw, s) & smask);
-        word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
-      }
-      slot[jw] = word;
-    }
-    return;
-  }
-
-  // ---- 7. encode (RFC 9639 9.2).  Code bits of each chunk from the exact pass's sums; bit position of
+  // ---- 7. encode (RFC 9639 9.2).  Code bits of each chunk from the exact pass's sums; the bit position of
   // every iteration's first code (B[j]) known up front
   const uint32_t fbits = (uint32_t)exact;
   const uint32_t nw = (fbits + 31) >> 5;
   const int pb = big ? 5 : 4;
-  uint32_t pos = hdr + (uint32_t)o * sbps + (type == 3 ? 9u + (uint32_t)o * prec : 0u);
+  const uint32_t pos = hdr + (uint32_t)o * sbps + (type == 3 ? 9u + (uint32_t)o * prec : 0u);
   uint32_t totl[kWIters];
   uint32_t B[kWIters + 1];
   B[0] = pos + 6;
@@ -870,44 +1019,66 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
     totl[j] = f + (uint32_t)(kChunk - (t == 0 ? o : 0)) * (kcur + 1u) + (pstart ? (uint32_t)pb : 0u);
     B[j + 1] = B[j] + wave_sum32(totl[j]);
   }
-  // The bit buffer aliases the samples and is filled iteration by iteration, each iteration's samples
-  // read (its residuals in registers) before its words are zeroed and written.  Iteration j must leave
-  // chunk 64 j + 63 intact (iteration j + 1 looks back into it): its last word + the spare one stay below
-  // that chunk's first word.  Otherwise (an incompressible start before a compressible rest)
-  // the codes go straight to the slot in global memory by atomic ORs.
-  bool safe = true;
+  // The bit buffer aliases the residuals and is filled iteration by iteration, each iteration's residuals
+  // read into registers before its words are zeroed and written: iteration j's last word + the spare one
+  // must stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a
+  // compressible rest -- the subframe goes to k_analyze).  Not smaller than VERBATIM: k_analyze too.
+  bool ok = exact < verb;
 #pragma unroll
-  for (int j = 0; j + 1 < kWIters; j++) safe = safe && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * j + 63, 0);
-  auto put_header = [&](uint32_t* buf) {
-    if (lane == 0) {
-      const int tcode = type == 2 ? 8 + o : 31 + o;
-      lds_put(buf, 0, (uint32_t)(tcode << 1) | (w ? 1u : 0u), 8);
-      if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
-    }
-    if (lane < o) lds_put(buf, hdr + (uint32_t)lane * sbps, (uint32_t)warm & smask, sbps);
-    uint32_t ph = hdr + (uint32_t)o * sbps;
-    if (type == 3) {
+  for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
+  if (!ok) {
+    hand_back(exact >= verb ? 6 : 7);
+    return;
+  }
+  if (lane < kMaxLpc) {
+    int32_t cv = 0;
+#pragma unroll
+    for (int jq = 0; jq < 8; jq++) cv = lane == jq ? wq[jq] : cv;
+    d->coef[lane] = type == 3 ? cv : 0;
+  }
+  if (lane == 0) {
+    d->wasted = (uint8_t)w; d->sbps = (uint8_t)sbps; d->cval = 0;
+    d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
+    d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh; d->bits = (uint32_t)exact;
+  }
+  const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
+  uint32_t* const buf = sw;
+  uint32_t Z = 0;  // words [0, Z) are zeroed (and possibly written)
+#pragma unroll
+  for (int j = 0; j < kWIters; j++) {
+    const int t = 64 * j + lane;
+    const bool head = t == 0;
+    uint32_t un[kChunk];
+    residuals(j, un);
+    wsync();  // every lane's reads of this iteration's residuals precede the zeroing
+    const uint32_t Zend = j == kWIters - 1 ? nw + 1 : (B[j + 1] - 1) / 32 + 2;
+    for (uint32_t jw = Z + lane; jw < Zend; jw += 64) buf[jw] = 0u;
+    Z = Zend > Z ? Zend : Z;
+    wsync();
+    if (j == 0) {  // subframe header, warm-up samples, qlp precision / shift / coefficients, residual header
       if (lane == 0) {
+        lds_put(buf, 0, (uint32_t)((type == 3 ? 31 + o : 8 + o) << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
+      }
+      if (lane < o) lds_put(buf, hdr + (uint32_t)lane * sbps, (uint32_t)warm & smask, sbps);
+      const uint32_t ph = hdr + (uint32_t)o * sbps;
+      if (type == 3 && lane == 0) {
         lds_put(buf, ph, (uint32_t)(prec - 1), 4);
         lds_put(buf, ph + 4, (uint32_t)sh & 31u, 5);
       }
-      if (lane < o) {
+      if (type == 3 && lane < o) {
         int32_t cv = 0;
 #pragma unroll
         for (int jq = 0; jq < 8; jq++) cv = lane == jq ? wq[jq] : cv;
         lds_put(buf, ph + 9 + (uint32_t)lane * prec, (uint32_t)cv & ((1u << prec) - 1u), prec);
       }
+      if (lane == 0) lds_put(buf, pos, ((uint32_t)(big ? 1 : 0) << 4) | (uint32_t)ps, 6);
     }
-    if (lane == 0) lds_put(buf, pos, ((uint32_t)(big ? 1 : 0) << 4) | (uint32_t)ps, 6);
-  };
-  auto put_codes = [&](uint32_t* buf, int j, const uint32_t (&un)[kChunk]) {
-    const int t = 64 * j + lane;
-    const bool head = t == 0;
-    const uint32_t kcur = sel4(kc, j), tot = sel4(totl, j);
+    const uint32_t kcur = kc[j], tot = totl[j];
     const bool pstart = ((t << 4) & (pz - 1)) == 0;
-    const uint32_t Bj = j == 0 ? B[0] : j == 1 ? B[1] : j == 2 ? B[2] : B[3];
-    uint32_t p = Bj + wave_incl_scan32(tot) - tot;
+    uint32_t p = B[j] + wave_incl_scan32(tot) - tot;
     if (pstart) { lds_put(buf, p, kcur, pb); p += (uint32_t)pb; }
+    // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
     const uint32_t sal = 31u - kcur;
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) {
@@ -917,43 +1088,33 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         p = Pp + 1u + kcur;
       }
     }
-  };
-  if (safe) {
-    uint32_t Z = 0;  // words [0, Z) are zeroed (and possibly written)
-#pragma unroll 1
-    for (int j = 0; j < kWIters; j++) {
-      uint32_t un[kChunk];
-      residuals(j, un);
-      wsync();  // every lane's reads of this iteration's samples are done
-      const uint32_t Bn = j == 0 ? B[1] : j == 1 ? B[2] : j == 2 ? B[3] : B[4];
-      const uint32_t Zend = j == kWIters - 1 ? nw + 1 : (Bn - 1) / 32 + 2;
-      for (uint32_t jw = Z + lane; jw < Zend; jw += 64) sw[jw] = 0u;
-      Z = Zend > Z ? Zend : Z;
-      wsync();
-      if (j == 0) put_header(sw);
-      put_codes(sw, j, un);
-    }
-    wsync();
-    for (uint32_t jw = lane; jw < nw; jw += 64) slot[jw] = sw[jw];
-  } else {
-    for (uint32_t jw = lane; jw <= nw; jw += 64) slot[jw] = 0u;  // (nw + 1 <= tmp_stride)
-    __threadfence();
-    put_header(slot);
-#pragma unroll 1
-    for (int j = 0; j < kWIters; j++) {
-      uint32_t un[kChunk];
-      residuals(j, un);
-      put_codes(slot, j, un);
-    }
   }
+  wsync();
+  for (uint32_t jw = lane; jw < nw; jw += 64) slot[jw] = buf[jw];
+  FRA_WSTAMP(8)
+  asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
 }
+
+#ifdef FRA_STAMPS
+}  // namespace fra
+extern "C" __attribute__((visibility("default"))) int fra_diag_wstamps(void* host, unsigned long long bytes) {
+  if (!host) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fra::g_fra_wstamps)) != hipSuccess) return -1;
+    return hipMemset(d, 0, sizeof(fra::g_fra_wstamps)) == hipSuccess ? 0 : -1;
+  }
+  const size_t nb = bytes < sizeof(fra::g_fra_wstamps) ? bytes : sizeof(fra::g_fra_wstamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(fra::g_fra_wstamps), nb, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+namespace fra {
+#endif
 
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s) {
   if (a.frame_count <= 0) return hipSuccess;
   const dim3 grid((unsigned)a.frame_count, (unsigned)cw);
   const LevelCfg cfg = level_cfg(level);
-  if (cfg.nsub == 0) k_analyze_w<0><<<grid, 64, 0, s>>>(a, src);
-  else k_analyze_w<8><<<grid, 64, 0, s>>>(a, src);
+  if (cfg.nsub == 0 || cfg.max_lpc > 8) return hipErrorInvalidValue;  // levels 3-6 only
+  k_analyze_w<8><<<grid, 64, 0, s>>>(a, src);
   return hipGetLastError();
 }
 

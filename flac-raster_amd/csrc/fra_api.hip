@@ -32,8 +32,8 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
                          hipStream_t s, int max_blocks);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, const int32_t* slow,
-                          int nslow);
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, int32_t* redo,
+                          unsigned* redo_count, int max_redo_blocks);
 hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
@@ -93,9 +93,11 @@ struct fra_plan {
   float* d_win = nullptr;
   int32_t* d_wrange = nullptr;
   int32_t* d_wplat = nullptr;
-  // frames whose block is shorter than kMaxBlock (ascending): k_analyze_w takes the full ones
-  std::vector<int32_t> slow;
-  int32_t* d_slow = nullptr;
+  // redo lists of k_analyze_w (subframes left to k_analyze): per buffer set, entries [frames x cmax] (a
+  // frame group / host band uses the entries of its own frames) and one counter per group slot
+  int32_t* d_redo[2] = {};
+  unsigned* d_redo_cnt[2] = {};
+  int redo_slots = 1;
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -308,7 +310,10 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_win);
   (void)hipFree(p->d_wrange);
   (void)hipFree(p->d_wplat);
-  (void)hipFree(p->d_slow);
+  for (int b = 0; b < 2; b++) {
+    (void)hipFree(p->d_redo[b]);
+    (void)hipFree(p->d_redo_cnt[b]);
+  }
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
     for (int b = 0; b < 2; b++) {
       (void)hipFree(p->sf2[b]);
@@ -577,14 +582,6 @@ static int plan_build(fra_plan* p) {
     HIPCHK(hipMalloc(&p->d_wplat, sizeof(int32_t) * wp.size()));
     HIPCHK(hipMemcpy(p->d_wplat, wp.data(), sizeof(int32_t) * wp.size(), hipMemcpyHostToDevice));
   }
-  {
-    p->slow.clear();
-    for (int f = 0; f < nfr; f++)
-      if (p->frames[f].n != kMaxBlock) p->slow.push_back(f);
-    HIPCHK(hipMalloc(&p->d_slow, sizeof(int32_t) * std::max<size_t>(1, p->slow.size())));
-    if (!p->slow.empty())
-      HIPCHK(hipMemcpy(p->d_slow, p->slow.data(), sizeof(int32_t) * p->slow.size(), hipMemcpyHostToDevice));
-  }
   if (!p->streams.empty())
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
   if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
@@ -631,6 +628,12 @@ static int plan_build(fra_plan* p) {
       hipStream_t st = nullptr;
       HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
       p->aux.push_back(st);
+    }
+    p->redo_slots = (int)std::max(p->groups.size(), p->hbands.size()) + 1;
+    if (!p->b32 && j.blocksize == kMaxBlock && j.level >= 3 && j.level <= 6 && j.norm != 0 &&
+        elem_size(j.dtype) <= 2 && j.dtype != FRA_F64) {  // plans k_analyze_w may take (wave_path)
+      HIPCHK(hipMalloc(&p->d_redo[0], sizeof(int32_t) * (size_t)std::max(1, nfr) * p->cmax));
+      HIPCHK(hipMalloc(&p->d_redo_cnt[0], sizeof(unsigned) * p->redo_slots));
     }
     p->gev.assign(1 + 2 * p->groups.size(), nullptr);
     for (auto& e : p->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -707,6 +710,10 @@ static int plan_build(fra_plan* p) {
       HIPCHK(hipMalloc(&p->fmeta2[1], sizeof(uint32_t) * kMetaWords * nfr));
       HIPCHK(hipMalloc(&p->fbytes2[1], sizeof(unsigned long long) * (nfr + 1)));
       HIPCHK(hipMalloc(&p->foff2[1], sizeof(unsigned long long) * (nfr + 1)));
+      if (p->d_redo[0]) {
+        HIPCHK(hipMalloc(&p->d_redo[1], sizeof(int32_t) * (size_t)std::max(1, nfr) * p->cmax));
+        HIPCHK(hipMalloc(&p->d_redo_cnt[1], sizeof(unsigned) * p->redo_slots));
+      }
       {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -846,12 +853,12 @@ static void collect_times(fra_plan* p) {
 }
 
 // k_analyze_w (one subframe per wave, fra_analyze_w.hip) takes the full frames of 16-bit plans normalised
-// through the per-tile table with 8-byte sample vectors at levels 0-6; FRA_ANALYZE_WG=1 keeps every frame on
-// the workgroup kernel (tests compare both)
+// through the per-tile table with 8-byte sample vectors at levels 3-6 (handing back to k_analyze what it does
+// not finish); FRA_ANALYZE_WG=1 keeps every frame on the workgroup kernel (tests compare both)
 static bool wave_path(const fra_plan* p) {
   const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
   return !wg && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&
-         p->job.level <= 6;
+         p->job.level >= 3 && p->job.level <= 6;
 }
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
@@ -888,15 +895,13 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
   {
-    const int32_t* slow = nullptr;
-    int nslow = 0;
-    if (wave_path(p)) {  // k_analyze_w for the full frames, k_analyze for this range's partial ones
-      const auto lo = std::lower_bound(p->slow.begin(), p->slow.end(), gr.f0);
-      const auto hi = std::lower_bound(lo, p->slow.end(), gr.f1);
-      slow = p->d_slow + (lo - p->slow.begin());
-      nslow = (int)(hi - lo);
-    }
-    HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, slow, nslow));
+    // k_analyze_w for the full frames, k_analyze for the subframes it hands back (this group's own redo
+    // entries and counter in the current buffer set)
+    const int b = p->cur;
+    const bool wave = wave_path(p) && p->d_redo[b];
+    HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, wave,
+                          wave ? p->d_redo[b] + (size_t)gr.f0 * p->cmax : nullptr,
+                          wave ? p->d_redo_cnt[b] + std::min(gi, p->redo_slots - 1) : nullptr, 8 * p->ncu));
   }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage

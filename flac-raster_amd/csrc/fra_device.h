@@ -955,6 +955,31 @@ __device__ __forceinline__ void load_window(const float* win, int i0, int n, flo
   }
 }
 
+// L2 prefetch hint (k_analyze, k_analyze_w): one dword per 128-byte line of the raw rows of the subframe DIST
+// blocks ahead in dispatch order (linear block id over the (frames, channels) grid; a multiple of 8 keeps
+// the same XCD, blocks being dealt round-robin over the XCDs).  Nothing depends on the words but the speed.
+template <typename T, int DIST>
+__device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {
+  const uint32_t nx = gridDim.x;
+  const uint64_t L = (uint64_t)blockIdx.x + (uint64_t)blockIdx.y * nx + DIST;
+  if (L >= (uint64_t)nx * gridDim.y) return 0u;
+  const int xp = (int)(L % nx), yp = (int)(L / nx);  // uniform
+  const FrameDev f2 = a.frames[a.frame_base + xp];
+  const StreamDev s2 = a.streams[f2.stream];
+  if (yp >= s2.channels || s2.ms || f2.n != kMaxBlock || s2.col_stride != 1) return 0u;
+  const char* b0 = (const char*)((const T*)a.raster + s2.base_off + (int64_t)yp * s2.band_stride +
+                                 (int64_t)f2.row0 * s2.row_stride);
+  const uint32_t w = (uint32_t)s2.width, rsb = (uint32_t)s2.row_stride * (uint32_t)sizeof(T);
+  // the 64-sample run of this lane (inside the subframe: n == 4096) spans <= 128 bytes: its first and
+  // last samples cover every line it touches (dword-aligned down)
+  auto word = [&](uint32_t c) -> uint32_t {
+    const uint32_t q = c / w;
+    return *(const uint32_t*)(b0 + ((q * rsb + (c - q * w) * (uint32_t)sizeof(T)) & ~3u));
+  };
+  const uint32_t c0 = (uint32_t)f2.col0 + 64u * (uint32_t)lane;
+  return word(c0) ^ word(c0 + 63u);
+}
+
 // ---------------------------------------------------------------- frame header (RFC 9639 9.1)
 __host__ __device__ inline int utf8_len(uint32_t v) {
   if (v < 0x80) return 1;

@@ -209,7 +209,8 @@ struct JobArgs {
                            // (k_analyze fast load path: 32-bit lane offsets from a uniform base)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
-  const int32_t* flist;    // k_analyze only: if set, workgroup x analyses frame flist[x] (frame_count of them)
+  int32_t* redo;           // k_analyze_w appends (frame * 8 + channel) of the subframes it leaves to k_analyze;
+  unsigned* redo_count;    //   k_analyze with redo set works through the list (null: the normal grid)
 };
 
 }  // namespace fra
