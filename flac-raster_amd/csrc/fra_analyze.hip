@@ -700,9 +700,19 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
           return;
         }
         // coefficients loaded here, not prefetched before the FIXED sums: a prefetch kept 16 + MAXLAG
-        // registers live through them and pushed the 7-wave instance into scratch
+        // registers live through them and pushed the 7-wave instance into scratch.  Inside the window's
+        // plateau of exact 1.0f (tukey and partial tukeys) the product is the sample itself:
+        // no load, and no multiply when the whole wave's span lies inside (bit-identical partials)
+        const int32_t* wpl = a.wplat + 2 * ((size_t)fr.win * a.nwin + wi);
+        const bool plat = i0 >= wpl[0] && i0 + kChunk + MAXLAG <= wpl[1];
         float wcoef[kChunk + MAXLAG];
-        load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
+        if (plat) {
+#pragma unroll
+          for (int j = 0; j < kChunk + MAXLAG; j++) wcoef[j] = 1.0f;
+        } else {
+          load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
+        }
+        const bool allplat = __all(plat);
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];
@@ -714,7 +724,7 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
           for (int j = 0; j < kChunk + MAXLAG; j++) {
             const int i = i0 + j;
             const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
-            wf[j] = (float)v * wcoef[j];
+            wf[j] = allplat ? (float)v : (float)v * wcoef[j];
           }
         }
 

@@ -486,6 +486,10 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
   uint32_t* const slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
 
+  // L2 prefetch of the rows of the subframe kWPrefetch waves ahead, issued first: its metadata loads overlap
+  // this wave's own, and its row loads land with this wave's (in-order vmcnt)
+  const uint32_t pf = (src == ST_U16 || src == ST_I16) ? prefetch_rows<uint16_t, kWPrefetch>(a, lane)
+                                                       : prefetch_rows<uint8_t, kWPrefetch>(a, lane);
   // ---- 1. load + normalise (table gather), OR / min / max
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
@@ -515,6 +519,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       slot[0] = (uint32_t)(blob >> 32);
       slot[1] = (uint32_t)blob;
     }
+    asm volatile("" ::"v"(pf));
     return;
   }
   const int w = __builtin_ctz(orv);
@@ -528,10 +533,6 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   };
   if (w) shift_wasted();
   wsync();
-  // L2 prefetch of the rows of the subframe kWPrefetch waves ahead (issued after this wave's own loads and
-  // gathers: nothing waits for it until the window coefficient loads, long after it landed)
-  const uint32_t pf = (src == ST_U16 || src == ST_I16) ? prefetch_rows<uint16_t, kWPrefetch>(a, lane)
-                                                       : prefetch_rows<uint8_t, kWPrefetch>(a, lane);
   const uint32_t hdr = 8u + (uint32_t)w;
   const uint32_t verb = hdr + (uint32_t)n * (uint32_t)sbps;
   const int P = max_porder(n, 0, cfg.max_porder);  // = cfg.max_porder (3..6)
@@ -829,48 +830,60 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   }
 
   FRA_WSTAMP(6)
-  // ---- 6. the winner's zig-zag residuals in LDS, int16 pairs in the samples' place: the kept ones, or (any
-  // other winner: a FIXED order, another window) the samples loaded again if the keep pass overwrote them
-  // and the winner's residuals written the same way.  Residuals past 16 bits, VERBATIM or an encode that would
-  // overrun its residuals in the aliased bit buffer: the subframe goes to k_analyze
+  // ---- 6. the winner's zig-zag residuals, exact Rice bits with each partition's parameter refined (3.9),
+  // encode (RFC 9639 9.2).  Two instances:
+  //  * kept (the common case): the winner is the LPC model of the keep pass and every residual fits 16 bits:
+  //    residuals read as int16 pairs from the samples' place, the bit buffer in LDS aliasing them;
+  //  * otherwise (a FIXED order, another window, residuals past 16 bits): the samples (loaded again if the keep
+  //    pass overwrote them) and the winner's predictor, the codes ORed straight into the slot in global memory.
+  // A kept subframe that is not smaller than VERBATIM, or whose encode would overrun its residuals in the
+  // aliased buffer, goes to k_analyze (redo list)
   const int type = wtype, o = wo, sh = wsh, ps = wps;
-  if (!(type == 3 && wm == 5 + keep_wi && kept_fit)) {
-    if (type == 3 && wm == 5 + keep_wi) {  // the kept model, but some residual needs more than 16 bits
-      hand_back(5);
-      return;
-    }
-    if (keep_wi >= 0) {
-      wsync();
-      uint32_t ov = 0;
-      int32_t mn = 0, mx = 0;
-      load_samples(ov, mn, mx);
-      if (w) shift_wasted();
-      wsync();
+  const bool kept_w = type == 3 && wm == 5 + keep_wi && kept_fit;
+  if (!kept_w && keep_wi >= 0) {  // the keep pass replaced the samples: load them once more
+    wsync();
+    uint32_t ov = 0;
+    int32_t mn = 0, mx = 0;
+    load_samples(ov, mn, mx);
+    if (w) shift_wasted();
+    wsync();
+  }
+  const int pz = n >> ps;
+  const int tl = 8 - ps;                  // log2 chunks per partition (2..8)
+  const int ls = tl < 6 ? tl : 6;         // lanes per partition group inside one iteration
+  const int npp = 1 << ps;
+  auto tail = [&](auto kept_tag) {
+    constexpr bool kept = decltype(kept_tag)::value;
+    int32_t warm = 0;  // warm-up sample `lane`
+    if (kept) {
+      const uint32_t wv2 = lane >= 6 ? w4[3] : lane >= 4 ? w4[2] : lane >= 2 ? w4[1] : w4[0];
+      warm = lane < o ? ((lane & 1) ? hi16(wv2) : lo16(wv2)) : 0;
+    } else if (lane < o) {
+      warm = wsample(sw, lane);
     }
     fra_short2 Q[4];
     q_pairs_rev<4>(wq, Q);
-    uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll 1
-    for (int j = 0; j < kWIters; j++) {
+    // the residuals of chunk 64 j + lane (warm-up positions 0)
+    auto residuals = [&](int j, uint32_t (&un)[kChunk]) {
       const int t = 64 * j + lane;
-      uint32_t* const po = sw + bo + kWIterDw * j;
+      if (kept) {  // 8 dwords of int16 pairs
+        const uint32_t* po = sw + bo + kWIterDw * j;
+#pragma unroll
+        for (int p = 0; p < kChunk / 4; p++) {
+          const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
+          un[4 * p] = v.x & 0xFFFFu;
+          un[4 * p + 1] = v.x >> 16;
+          un[4 * p + 2] = v.y & 0xFFFFu;
+          un[4 * p + 3] = v.y >> 16;
+        }
+        return;
+      }
       uint32_t D[14];
-      wread_d14(po, sw + bpv + kWIterDw * j, D);
-      if (j > 0) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) D[k] = lane == 0 ? carry[k] : D[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; k++) carry[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[8 + k], 63);
-      if (j == 0) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) w4[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[6 + k], 0);
-      }
-      uint32_t u[kChunk];
+      wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
       if (type == 3) {
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) u[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
-      } else {  // FIXED: the o-th finite difference
+        for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
+      } else {  // FIXED: the o-th finite difference in place
         int32_t x[28];
         unpack28(D, x);
 #pragma unroll
@@ -881,181 +894,174 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           }
         }
 #pragma unroll
-        for (int jj = 0; jj < kChunk; jj++) u[jj] = zz32(x[12 + jj]);
+        for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(x[12 + jj]);
       }
 #pragma unroll
       for (int jj = 0; jj < 12; jj++)
-        if (t == 0 && jj < o) u[jj] = 0u;
+        if (t == 0 && jj < o) un[jj] = 0u;
+    };
+    uint32_t kc[kWIters];       // Rice parameter of the lane's chunk of iteration j
+    uint32_t fk[kWIters][3];    // sums of u >> (k0 - 1), u >> k0, u >> (k0 + 1) of that chunk
+    uint32_t k0r[kWIters];
+    uint32_t bitsl = 0;         // exact bits of the partitions this lane leads
+    bool bigl = false;
+    uint64_t E[3] = {0, 0, 0};  // partitions spanning iterations (ps <= 1): running sums
 #pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) um |= u[jj];
-      wsync();
+    for (int j = 0; j < kWIters; j++) {
+      const int t = 64 * j + lane;
+      uint32_t un[kChunk];
+      residuals(j, un);
+      const int pidx = t >> tl;
+      const int k0 = __shfl((int)wk, pidx & 63, 64);
+      const int km = k0 > 0 ? k0 - 1 : 0;
+      uint32_t f0 = 0, f1 = 0, f2 = 0;  // u < 2^28: 16 of them fit 32 bits
 #pragma unroll
-      for (int p = 0; p < kChunk / 4; p++)
-        *reinterpret_cast<uint2*>(po + 2 * p) = make_uint2((u[4 * p + 1] << 16) | (u[4 * p] & 0xFFFFu),
-                                                           (u[4 * p + 3] << 16) | (u[4 * p + 2] & 0xFFFFu));
+      for (int jj = 0; jj < kChunk; jj++) {
+        f0 += un[jj] >> km;
+        f1 += un[jj] >> k0;
+        f2 += un[jj] >> (k0 + 1);
+      }
+      fk[j][0] = f0;
+      fk[j][1] = f1;
+      fk[j][2] = f2;
+      k0r[j] = (uint32_t)k0;
+      uint64_t v0, v1, v2;
+      if (kept || __all(f0 <= (0xFFFFFFFFu >> ls))) {  // (kept: u < 2^16, so <= 64 lanes fit 32 bits)
+        v0 = group_sum32(f0, ls); v1 = group_sum32(f1, ls); v2 = group_sum32(f2, ls);
+      } else {
+        v0 = group_sum64(f0, ls); v1 = group_sum64(f1, ls); v2 = group_sum64(f2, ls);
+      }
+      if (tl <= 6) {  // the partition lies inside this iteration: its last lane decides
+        int bk = 0;
+        if ((lane & ((1 << ls) - 1)) == (1 << ls) - 1) {
+          const uint64_t cnt = (uint64_t)(pz - (pidx == 0 ? o : 0));
+          const uint64_t ev[3] = {v0, v1, v2};
+          uint64_t best = 0;
+          bool first = true;
+#pragma unroll
+          for (int dk = -1; dk <= 1; dk++) {
+            const int kk = k0 + dk;
+            if (kk < 0 || kk > 30) continue;
+            const uint64_t e = cnt * (uint64_t)(kk + 1) + ev[dk + 1];
+            if (first || e < best) { best = e; bk = kk; first = false; }
+          }
+          bitsl += (uint32_t)best;
+          bigl = bigl || bk > 14;
+          d->k[pidx] = (uint8_t)bk;
+        }
+        kc[j] = (uint32_t)__shfl(bk, lane | ((1 << ls) - 1), 64);
+      } else {  // ps <= 1: whole-iteration sums accumulate into the partition's running sums (uniform)
+        auto rl64 = [](uint64_t v) -> uint64_t {
+          return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32);
+        };
+        E[0] += rl64(v0);
+        E[1] += rl64(v1);
+        E[2] += rl64(v2);
+        const int span = 1 << (tl - 6);  // iterations per partition (2 or 4)
+        kc[j] = 0;
+        if (((j + 1) & (span - 1)) == 0) {  // partition complete: decide its parameter
+          const int pq = j >> (tl - 6);
+          const uint64_t cnt = (uint64_t)(pz - (pq == 0 ? o : 0));
+          int bk = 0;
+          uint64_t best = 0;
+          bool first = true;
+#pragma unroll
+          for (int dk = -1; dk <= 1; dk++) {
+            const int kk = k0 + dk;
+            if (kk < 0 || kk > 30) continue;
+            const uint64_t e = cnt * (uint64_t)(kk + 1) + E[dk + 1];
+            if (first || e < best) { best = e; bk = kk; first = false; }
+          }
+          if (lane == 0) {
+            bitsl += (uint32_t)best;
+            d->k[pq] = (uint8_t)bk;
+          }
+          bigl = bigl || bk > 14;
+#pragma unroll
+          for (int jx = 0; jx < kWIters; jx++)
+            if (jx <= j && jx > j - span) kc[jx] = (uint32_t)bk;
+          E[0] = E[1] = E[2] = 0;
+        }
+      }
     }
-    if (__any(um > 0xFFFFu)) {
-      hand_back(type == 3 ? 4 : 3);
+    FRA_WSTAMP(7)
+    const bool big = __any(bigl);
+    const uint64_t rtot = (uint64_t)wave_sum32(bitsl) + (uint64_t)npp * (big ? 5 : 4) + 6;
+    const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
+    const bool verbatim = exact >= verb;
+    const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
+    if (kept && verbatim) {
+      hand_back(6);
+      asm volatile("" ::"v"(pf));
       return;
     }
-  }
-  const int pz = n >> ps;
-  const int tl = 8 - ps;                  // log2 chunks per partition (2..8)
-  const int ls = tl < 6 ? tl : 6;         // lanes per partition group inside one iteration
-  const int npp = 1 << ps;
-  int32_t warm;                           // warm-up sample `lane` (saved by the keep pass)
-  {
-    const uint32_t wv2 = lane >= 6 ? w4[3] : lane >= 4 ? w4[2] : lane >= 2 ? w4[1] : w4[0];
-    warm = lane < o ? ((lane & 1) ? hi16(wv2) : lo16(wv2)) : 0;
-  }
-  // the residuals of chunk 64 j + lane (warm-up positions 0): its 8 dwords of int16 pairs
-  auto residuals = [&](int j, uint32_t (&un)[kChunk]) {
-    const uint32_t* po = sw + bo + kWIterDw * j;
-#pragma unroll
-    for (int p = 0; p < kChunk / 4; p++) {
-      const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
-      un[4 * p] = v.x & 0xFFFFu;
-      un[4 * p + 1] = v.x >> 16;
-      un[4 * p + 2] = v.y & 0xFFFFu;
-      un[4 * p + 3] = v.y >> 16;
-    }
-  };
-  uint32_t kc[kWIters];       // Rice parameter of the lane's chunk of iteration j
-  uint32_t fk[kWIters][3];    // sums of u >> (k0 - 1), u >> k0, u >> (k0 + 1) of that chunk (u < 2^16)
-  uint32_t k0r[kWIters];
-  uint32_t bitsl = 0;         // exact bits of the partitions this lane leads
-  bool bigl = false;
-  uint64_t E[3] = {0, 0, 0};  // partitions spanning iterations (ps <= 1): running sums
-#pragma unroll
-  for (int j = 0; j < kWIters; j++) {
-    const int t = 64 * j + lane;
-    uint32_t un[kChunk];
-    residuals(j, un);
-    const int pidx = t >> tl;
-    const int k0 = __shfl((int)wk, pidx & 63, 64);
-    const int km = k0 > 0 ? k0 - 1 : 0;
-    uint32_t f0 = 0, f1 = 0, f2 = 0;
-#pragma unroll
-    for (int jj = 0; jj < kChunk; jj++) {
-      f0 += un[jj] >> km;
-      f1 += un[jj] >> k0;
-      f2 += un[jj] >> (k0 + 1);
-    }
-    fk[j][0] = f0;
-    fk[j][1] = f1;
-    fk[j][2] = f2;
-    k0r[j] = (uint32_t)k0;
-    // 16 u < 2^16 per lane: the group sums of <= 64 lanes fit 32 bits
-    const uint32_t v0 = group_sum32(f0, ls), v1 = group_sum32(f1, ls), v2 = group_sum32(f2, ls);
-    if (tl <= 6) {  // the partition lies inside this iteration: its last lane decides
-      int bk = 0;
-      if ((lane & ((1 << ls) - 1)) == (1 << ls) - 1) {
-        const uint64_t cnt = (uint64_t)(pz - (pidx == 0 ? o : 0));
-        const uint32_t ev[3] = {v0, v1, v2};
-        uint64_t best = 0;
-        bool first = true;
-#pragma unroll
-        for (int dk = -1; dk <= 1; dk++) {
-          const int kk = k0 + dk;
-          if (kk < 0 || kk > 30) continue;
-          const uint64_t e = cnt * (uint64_t)(kk + 1) + ev[dk + 1];
-          if (first || e < best) { best = e; bk = kk; first = false; }
-        }
-        bitsl += (uint32_t)best;
-        bigl = bigl || bk > 14;
-        d->k[pidx] = (uint8_t)bk;
+    if (!kept && verbatim) {  // straight from the samples to the slot
+      if (lane == 0) {
+        d->type = 1; d->order = 0; d->wasted = (uint8_t)w; d->sbps = (uint8_t)sbps; d->cval = 0; d->porder = 0;
+        d->method = 0; d->precision = 0; d->shift = 0; d->bits = verb;
       }
-      kc[j] = (uint32_t)__shfl(bk, lane | ((1 << ls) - 1), 64);
-    } else {  // ps <= 1: whole-iteration sums accumulate into the partition's running sums (uniform)
-      E[0] += (uint32_t)__builtin_amdgcn_readlane((int)v0, 63);
-      E[1] += (uint32_t)__builtin_amdgcn_readlane((int)v1, 63);
-      E[2] += (uint32_t)__builtin_amdgcn_readlane((int)v2, 63);
-      const int span = 1 << (tl - 6);  // iterations per partition (2 or 4)
-      kc[j] = 0;
-      if (((j + 1) & (span - 1)) == 0) {  // partition complete: decide its parameter
-        const int pq = j >> (tl - 6);
-        const uint64_t cnt = (uint64_t)(pz - (pq == 0 ? o : 0));
-        int bk = 0;
-        uint64_t best = 0;
-        bool first = true;
-#pragma unroll
-        for (int dk = -1; dk <= 1; dk++) {
-          const int kk = k0 + dk;
-          if (kk < 0 || kk > 30) continue;
-          const uint64_t e = cnt * (uint64_t)(kk + 1) + E[dk + 1];
-          if (first || e < best) { best = e; bk = kk; first = false; }
+      const uint32_t nwv = (verb + 31) >> 5;
+      const uint64_t hv = ((uint64_t)(2u | (w ? 1u : 0u)) << 56) | (w ? (1ull << (63 - (8 + w - 1))) : 0ull);
+      for (uint32_t jw = lane; jw < nwv; jw += 64) {
+        const int64_t wb = 32 * (int64_t)jw;
+        uint32_t word = jw == 0 ? (uint32_t)(hv >> 32) : (jw == 1 ? (uint32_t)hv : 0u);
+        const int s0 = wb > (int64_t)hdr ? (int)((wb - (int64_t)hdr) / sbps) : 0;
+        for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
+          const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
+          const int sft = 32 - (int)rel - sbps;
+          const uint64_t v = (uint64_t)((uint32_t)wsample(sw, s) & smask);
+          word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
         }
-        if (lane == 0) {
-          bitsl += (uint32_t)best;
-          d->k[pq] = (uint8_t)bk;
-        }
-        bigl = bigl || bk > 14;
+        slot[jw] = word;
+      }
+      asm volatile("" ::"v"(pf));
+      return;
+    }
+    // code bits of each chunk from the exact pass's sums; the bit position of every iteration's first code
+    const uint32_t fbits = (uint32_t)exact;
+    const uint32_t nw = (fbits + 31) >> 5;
+    const int pb = big ? 5 : 4;
+    const uint32_t pos = hdr + (uint32_t)o * sbps + (type == 3 ? 9u + (uint32_t)o * prec : 0u);
+    uint32_t totl[kWIters];
+    uint32_t B[kWIters + 1];
+    B[0] = pos + 6;
 #pragma unroll
-        for (int jx = 0; jx < kWIters; jx++)
-          if (jx <= j && jx > j - span) kc[jx] = (uint32_t)bk;
-        E[0] = E[1] = E[2] = 0;
+    for (int j = 0; j < kWIters; j++) {
+      const int t = 64 * j + lane;
+      const uint32_t kcur = kc[j], k0 = k0r[j];
+      const uint32_t f = kcur + 1 == k0 ? fk[j][0] : kcur == k0 ? fk[j][1] : fk[j][2];
+      const bool pstart = ((t << 4) & (pz - 1)) == 0;
+      totl[j] = f + (uint32_t)(kChunk - (t == 0 ? o : 0)) * (kcur + 1u) + (pstart ? (uint32_t)pb : 0u);
+      B[j + 1] = B[j] + wave_sum32(totl[j]);
+    }
+    if (kept) {
+      // the LDS bit buffer aliases the residuals and is filled iteration by iteration, each iteration's
+      // residuals read before its words are zeroed and written: iteration j's last word + the spare one must
+      // stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a compressible
+      // rest -- the subframe goes to k_analyze)
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
+      if (!ok) {
+        hand_back(7);
+        asm volatile("" ::"v"(pf));
+        return;
       }
     }
-  }
-  FRA_WSTAMP(7)
-  const bool big = __any(bigl);
-  const uint64_t rtot = (uint64_t)wave_sum32(bitsl) + (uint64_t)npp * (big ? 5 : 4) + 6;
-  const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
-  // ---- 7. encode (RFC 9639 9.2).  Code bits of each chunk from the exact pass's sums; the bit position of
-  // every iteration's first code (B[j]) known up front
-  const uint32_t fbits = (uint32_t)exact;
-  const uint32_t nw = (fbits + 31) >> 5;
-  const int pb = big ? 5 : 4;
-  const uint32_t pos = hdr + (uint32_t)o * sbps + (type == 3 ? 9u + (uint32_t)o * prec : 0u);
-  uint32_t totl[kWIters];
-  uint32_t B[kWIters + 1];
-  B[0] = pos + 6;
+    if (lane < kMaxLpc) {
+      int32_t cv = 0;
 #pragma unroll
-  for (int j = 0; j < kWIters; j++) {
-    const int t = 64 * j + lane;
-    const uint32_t kcur = kc[j], k0 = k0r[j];
-    const uint32_t f = kcur + 1 == k0 ? fk[j][0] : kcur == k0 ? fk[j][1] : fk[j][2];
-    const bool pstart = ((t << 4) & (pz - 1)) == 0;
-    totl[j] = f + (uint32_t)(kChunk - (t == 0 ? o : 0)) * (kcur + 1u) + (pstart ? (uint32_t)pb : 0u);
-    B[j + 1] = B[j] + wave_sum32(totl[j]);
-  }
-  // The bit buffer aliases the residuals and is filled iteration by iteration, each iteration's residuals
-  // read into registers before its words are zeroed and written: iteration j's last word + the spare one
-  // must stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a
-  // compressible rest -- the subframe goes to k_analyze).  Not smaller than VERBATIM: k_analyze too.
-  bool ok = exact < verb;
-#pragma unroll
-  for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
-  if (!ok) {
-    hand_back(exact >= verb ? 6 : 7);
-    return;
-  }
-  if (lane < kMaxLpc) {
-    int32_t cv = 0;
-#pragma unroll
-    for (int jq = 0; jq < 8; jq++) cv = lane == jq ? wq[jq] : cv;
-    d->coef[lane] = type == 3 ? cv : 0;
-  }
-  if (lane == 0) {
-    d->wasted = (uint8_t)w; d->sbps = (uint8_t)sbps; d->cval = 0;
-    d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
-    d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh; d->bits = (uint32_t)exact;
-  }
-  const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
-  uint32_t* const buf = sw;
-  uint32_t Z = 0;  // words [0, Z) are zeroed (and possibly written)
-#pragma unroll
-  for (int j = 0; j < kWIters; j++) {
-    const int t = 64 * j + lane;
-    const bool head = t == 0;
-    uint32_t un[kChunk];
-    residuals(j, un);
-    wsync();  // every lane's reads of this iteration's residuals precede the zeroing
-    const uint32_t Zend = j == kWIters - 1 ? nw + 1 : (B[j + 1] - 1) / 32 + 2;
-    for (uint32_t jw = Z + lane; jw < Zend; jw += 64) buf[jw] = 0u;
-    Z = Zend > Z ? Zend : Z;
-    wsync();
-    if (j == 0) {  // subframe header, warm-up samples, qlp precision / shift / coefficients, residual header
+      for (int jq = 0; jq < 8; jq++) cv = lane == jq ? wq[jq] : cv;
+      d->coef[lane] = type == 3 ? cv : 0;
+    }
+    if (lane == 0) {
+      d->wasted = (uint8_t)w; d->sbps = (uint8_t)sbps; d->cval = 0;
+      d->type = (uint8_t)type; d->order = (uint8_t)o; d->porder = (uint8_t)ps; d->method = big ? 1 : 0;
+      d->precision = (uint8_t)(type == 3 ? prec : 0); d->shift = (int8_t)sh; d->bits = (uint32_t)exact;
+    }
+    // subframe header, warm-up samples, qlp precision / shift / coefficients, residual coding method + order
+    auto put_header = [&](uint32_t* buf) {
       if (lane == 0) {
         lds_put(buf, 0, (uint32_t)((type == 3 ? 31 + o : 8 + o) << 1) | (w ? 1u : 0u), 8);
         if (w) lds_put(buf, 8 + (uint32_t)(w - 1), 1u, 1);
@@ -1073,26 +1079,59 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         lds_put(buf, ph + 9 + (uint32_t)lane * prec, (uint32_t)cv & ((1u << prec) - 1u), prec);
       }
       if (lane == 0) lds_put(buf, pos, ((uint32_t)(big ? 1 : 0) << 4) | (uint32_t)ps, 6);
-    }
-    const uint32_t kcur = kc[j], tot = totl[j];
-    const bool pstart = ((t << 4) & (pz - 1)) == 0;
-    uint32_t p = B[j] + wave_incl_scan32(tot) - tot;
-    if (pstart) { lds_put(buf, p, kcur, pb); p += (uint32_t)pb; }
-    // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
-    const uint32_t sal = 31u - kcur;
+    };
+    // the partition parameter (in front of a partition's first chunk) and the lane's 16 Rice codes
+    auto put_codes = [&](uint32_t* buf, int j, const uint32_t (&un)[kChunk]) {
+      const int t = 64 * j + lane;
+      const bool head = t == 0;
+      const uint32_t kcur = kc[j], tot = totl[j];
+      const bool pstart = ((t << 4) & (pz - 1)) == 0;
+      uint32_t p = B[j] + wave_incl_scan32(tot) - tot;
+      if (pstart) { lds_put(buf, p, kcur, pb); p += (uint32_t)pb; }
+      // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
+      const uint32_t sal = 31u - kcur;
 #pragma unroll
-    for (int jj = 0; jj < kChunk; jj++) {
-      if (!(jj < 12 && head && jj < o)) {
-        const uint32_t Pp = p + (un[jj] >> kcur);
-        lds_put_al(buf, Pp, (un[jj] << sal) | 0x80000000u);
-        p = Pp + 1u + kcur;
+      for (int jj = 0; jj < kChunk; jj++) {
+        if (!(jj < 12 && head && jj < o)) {
+          const uint32_t Pp = p + (un[jj] >> kcur);
+          lds_put_al(buf, Pp, (un[jj] << sal) | 0x80000000u);
+          p = Pp + 1u + kcur;
+        }
+      }
+    };
+    if (kept) {
+      uint32_t* const buf = sw;
+      uint32_t Z = 0;  // words [0, Z) are zeroed (and possibly written)
+#pragma unroll
+      for (int j = 0; j < kWIters; j++) {
+        uint32_t un[kChunk];
+        residuals(j, un);
+        wsync();  // every lane's reads of this iteration's residuals precede the zeroing
+        const uint32_t Zend = j == kWIters - 1 ? nw + 1 : (B[j + 1] - 1) / 32 + 2;
+        for (uint32_t jw = Z + lane; jw < Zend; jw += 64) buf[jw] = 0u;
+        Z = Zend > Z ? Zend : Z;
+        wsync();
+        if (j == 0) put_header(buf);
+        put_codes(buf, j, un);
+      }
+      wsync();
+      for (uint32_t jw = lane; jw < nw; jw += 64) slot[jw] = buf[jw];
+      FRA_WSTAMP(8)
+    } else {  // the samples stay: codes ORed into the zeroed slot (global atomics)
+      for (uint32_t jw = lane; jw <= nw; jw += 64) slot[jw] = 0u;  // (nw + 1 <= tmp_stride)
+      __threadfence();
+      put_header(slot);
+#pragma unroll 1
+      for (int j = 0; j < kWIters; j++) {
+        uint32_t un[kChunk];
+        residuals(j, un);
+        put_codes(slot, j, un);
       }
     }
-  }
-  wsync();
-  for (uint32_t jw = lane; jw < nw; jw += 64) slot[jw] = buf[jw];
-  FRA_WSTAMP(8)
-  asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
+    asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
+  };
+  if (kept_w) tail(std::true_type{});
+  else tail(std::false_type{});
 }
 
 #ifdef FRA_STAMPS
