@@ -464,7 +464,7 @@ def main():
         sh = {"shard": f"{shard_of[0]}/{shard_of[1]}", "config": cfg["workload"], "tiles": len(my_wins),
               "pixels": my_px, "ms_per_step": round(T / args.steps * 1e3, 4),
               "kernel_ms_per_launch": {"minmax": round(per_launch_ms[0], 4), "analyze": round(per_launch_ms[1], 4),
-                                       "frame_bytes+scan": round(per_launch_ms[2], 4),
+                                       "frame_scan": round(per_launch_ms[2], 4),
                                        "pack": round(per_launch_ms[3], 4)},
               "fixed_ms_per_step": round(T / args.steps * 1e3 - per_launch_ms[1], 4),
               "projected_job_mpix_s": round(H * W / (T / args.steps) / 1e6, 2),
@@ -495,7 +495,10 @@ def main():
                    "sample": f"first {cb['tiles']} tiles ({cb['pixels']} px, {cb['seconds']:.1f} s) of the same "
                              f"scene through oracle/fr_oracle.c normalize+encode (FRA-1, 1 thread, "
                              f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}); "
-                             f"bytes equal to GPU for {cb['checked'] - cb['mismatches']}/{cb['checked']} tiles"}
+                             f"bytes equal to GPU for {cb['checked'] - cb['mismatches']}/{cb['checked']} tiles. "
+                             f"Plain scalar C restatement of FRA-1, slower than the reference's numpy "
+                             f"normalisation alone (19.3 MPix/s per C4 tile, BASELINE.md 1): not a proxy for "
+                             f"libFLAC or the reference CPU path (measurable only if `reference_cpu` finds pyflac / flac)"}
             # B-mp: the same port over the host's core share (OMP_NUM_THREADS on the box = its CPU share)
             procs = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
             px_per_tile = cb["pixels"] / max(1, cb["tiles"])
@@ -587,7 +590,7 @@ def main():
                          "alg_bytes_per_launch": int(alg_bytes),
                          "kernel_ms_per_launch": {"minmax": round(per_launch_ms[0], 4),
                                                   "analyze": round(per_launch_ms[1], 4),
-                                                  "frame_bytes+scan": round(per_launch_ms[2], 4),
+                                                  "frame_scan": round(per_launch_ms[2], 4),
                                                   "pack": round(per_launch_ms[3], 4)},
                          "counters": pm,
                          "valu_note": f"valu_issue_frac = SQ_INSTS_VALU x {VALU_CYC} cyc / ({SIMDS} SIMDs x "

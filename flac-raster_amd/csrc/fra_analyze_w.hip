@@ -20,12 +20,10 @@
 // k_analyze, so every FRA-1 reduction order (the chunk-partial tree per 64 chunks, then
 // (G0 + G1) + (G2 + G3)) is unchanged.
 //
-// LDS per wave (9.6 KiB, 64-thread workgroups): the int16 samples in chunks of 8 dwords, dword d of chunk
-// t at 8 + 8t + 2 (t >> 3) + d (2 pad dwords per 8 chunks: the 8-byte reads of 32 lanes at a 32-byte
-// stride hit 64 distinct banks; d stays an immediate offset), a zero chunk in front (samples before the block)
-// and a spare one behind (look-ahead of the last chunk, multiplied by zero window coefficients); the
-// encoded subframe's bit buffer aliases the samples once the winner's residuals are in registers; a
-// 1.25 KiB scratch holds partition sums and the partition-search nodes.
+// LDS per wave: only the 4,096 int16 samples (8 KiB, so 20 waves fit a CU); partition sums and the
+// partition-search tree move between lanes by ds_bpermute / DPP, the LPC models live in scalar registers.
+// The winner's zig-zag residuals overwrite the samples in place (16-bit pairs), and the encoded subframe's
+// bit buffer then aliases them, filled iteration by iteration.
 #include <type_traits>
 
 #include "fra_device.h"
@@ -37,15 +35,14 @@ namespace {
 constexpr int kWChunks = kMaxBlock / kChunk;  // 256
 constexpr int kWIters = kWChunks / 64;        // chunks per lane
 
+// LDS per wave: exactly the 4,096 int16 samples (8 KiB: 20 waves per CU), chunk t (16 samples) at dwords
+// [8t, 8t + 8).  The bit buffer aliases them (<= 2,047 words + one spare; a longer subframe goes to the redo list)
 struct WaveSmem {
-  uint32_t sw[8 + 8 * (kWChunks + 1) + 2 * (kWChunks / 8)];  // zero chunk, 256 chunks (+ pads), spare chunk
-  unsigned long long scr[160];          // FIXED partition sums (u32 [5][64]) / LPC sums / search nodes
-  int32_t mdl[3][12];                   // LPC model of window wi: q[0..7], shift, order, ok
+  uint32_t sw[8 * kWChunks];
 };
-// the bit buffer: <= 2,049 words (exact < verbatim = 8 + 65,536 bits) + one spare zeroed word
-static_assert(sizeof(WaveSmem::sw) >= 4 * 2050, "bit buffer inside the sample array");
+constexpr uint32_t kBufWords = 8 * kWChunks;
 
-__device__ __forceinline__ int sdw(int t, int d) { return 8 + 8 * t + 2 * (t >> 3) + d; }
+__device__ __forceinline__ int sdw(int t, int d) { return 8 * t + d; }
 __device__ __forceinline__ int32_t wsample(const uint32_t* sw, int s) {
   const uint32_t v = sw[sdw(s >> 4, (s & 15) >> 1)];
   return (s & 1) ? hi16(v) : lo16(v);
@@ -56,28 +53,28 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
-// D[0..5] = the last 12 samples of chunk t - 1, D[6..13] = chunk t (int16 pairs, sample 16t - 12 + 2k in
-// the low half of D[k]) -- the layout read_d14 gives k_analyze
-// Chunk t = 64 j + lane starts at dword own(lane) + 528 j (528 = 64 chunks of 8 + 8 pads); its predecessor
-// at prev(lane) + 528 j, its successor at next(lane) + 528 j.  Every sample read is one of these three
-// per-lane bases + 528 j + an immediate offset (no per-access address registers)
-constexpr int kWIterDw = 8 * 64 + 2 * 8;
-__device__ __forceinline__ int base_own(int lane) { return 8 + 8 * lane + 2 * (lane >> 3); }
-__device__ __forceinline__ int base_prev(int lane) { return 8 * lane + 2 * ((lane - 1) >> 3); }
-__device__ __forceinline__ int base_next(int lane) { return 16 + 8 * lane + 2 * ((lane + 1) >> 3); }
-__device__ __forceinline__ void wread_d14(const uint32_t* po, const uint32_t* pp, uint32_t (&D)[14]) {
-#pragma unroll
-  for (int p = 0; p < 3; p++) {
-    const uint2 v = *reinterpret_cast<const uint2*>(pp + 2 + 2 * p);
-    D[2 * p] = v.x;
-    D[2 * p + 1] = v.y;
-  }
-#pragma unroll
-  for (int p = 0; p < 4; p++) {
-    const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
-    D[6 + 2 * p] = v.x;
-    D[7 + 2 * p] = v.y;
-  }
+// Chunk t = 64 j + lane starts at dword 8 lane + 512 j: every sample read is a per-lane base + 512 j + an
+// immediate offset, 16 bytes at a time (ds_read_b128: 16 lanes per LDS cycle at a 32-byte stride, 2-way)
+constexpr int kWIterDw = 8 * 64;
+constexpr int kWinW = 3;  // apodization windows of levels 3-6
+__device__ __forceinline__ uint4 lds4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+// D[0..5] = the last 12 samples of chunk t - 1 (zeros before the block: t == 0), D[6..13] = chunk t (int16
+// pairs, sample 16t - 12 + 2k in the low half of D[k]) -- the layout read_d14 gives k_analyze
+__device__ __forceinline__ void wread_d14(const uint32_t* sw, int lane, int j, uint32_t (&D)[14]) {
+  const uint32_t* po = sw + 8 * lane + kWIterDw * j;
+  const bool first = j == 0 && lane == 0;
+  const uint32_t* pp = first ? po : po - 8;  // (a valid address; zeroed below)
+  const uint4 p0 = lds4(pp), p1 = lds4(pp + 4), o0 = lds4(po), o1 = lds4(po + 4);
+  D[0] = first ? 0u : p0.z; D[1] = first ? 0u : p0.w;
+  D[2] = first ? 0u : p1.x; D[3] = first ? 0u : p1.y; D[4] = first ? 0u : p1.z; D[5] = first ? 0u : p1.w;
+  D[6] = o0.x; D[7] = o0.y; D[8] = o0.z; D[9] = o0.w;
+  D[10] = o1.x; D[11] = o1.y; D[12] = o1.z; D[13] = o1.w;
+}
+__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src) {  // lane src's v (ds_bpermute)
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src) {
+  return ((uint64_t)bperm32((uint32_t)(v >> 32), src) << 32) | bperm32((uint32_t)v, src);
 }
 __device__ __forceinline__ void unpack28(const uint32_t (&D)[14], int32_t (&x)[28]) {
 #pragma unroll
@@ -236,66 +233,63 @@ __device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, i
   g2 = __builtin_amdgcn_readfirstlane(h2);
 }
 
-// porder_search (fra_analyze.hip) on a register of finest partition sums (lane p < 2^P), node sums in the
-// wave's scratch; returns the best total, its order and, in kreg lane j < 2^bp, partition j's Rice parameter
-__device__ __forceinline__ void porder_search_w(uint64_t Sv, unsigned long long* node, int P, int pm, int n, int o,
-                                                int lane, uint64_t& best_out, int& bp_out, uint32_t& kreg) {
-  const bool narrow = __all(Sv < (1ull << 23));
+// porder_search (fra_analyze.hip) on a register of finest partition sums (lane p < 2^P), without LDS: node
+// (level q, index j) -- the sum of finest partitions [j 2^(P-q), (j+1) 2^(P-q)) -- is needed at lane 2^q + j;
+// the upper-lane tree leaves it after step P - q - 1 at lane (j+1) 2^(P-q) - 1, one ds_bpermute per step.
+// Same nodes, tree, tie rule and outputs as porder_search; kreg lane j < 2^bp = partition j's Rice parameter
+__device__ __forceinline__ void porder_search_w(uint64_t Sv, int P, int pm, int n, int o, int lane, uint64_t& best_out,
+                                                int& bp_out, uint32_t& kreg) {
+  const int p = lane ? 31 - __clz(lane) : 0;  // this lane's level; j = lane - 2^p
+  const int jn = lane - (1 << p);
   uint32_t bits32 = 0;
   bool big = false;
   int kn = 0;
-  const int p = lane ? 31 - __clz(lane) : 0;
   uint32_t tot6 = 0;
   bool big6 = false;
   int k6 = 0;
-  if (narrow) {  // every node sum < 2^29: 32-bit arithmetic (rice_pick32), bit-identical
-    uint32_t* nd = reinterpret_cast<uint32_t*>(node);
+  if (__all(Sv < (1ull << 23))) {  // every node sum < 2^29: 32-bit arithmetic (rice_pick32), bit-identical
     uint32_t S = (uint32_t)Sv;
-    if (lane < (1 << P)) nd[(1 << P) + lane] = S;
+    uint32_t nv = p == P ? bperm32(S, jn) : 0u;  // level P <= 5: the finest sums themselves
 #define FRA_NODE_STEP32(S_)                                                        \
   if (P > S_) {                                                                    \
     S = up_add32<S_>(S);                                                           \
-    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
-      nd[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = S;                            \
+    const uint32_t tv = bperm32(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
+    nv = p == P - S_ - 1 ? tv : nv;                                                \
   }
     FRA_NODE_STEP32(0) FRA_NODE_STEP32(1) FRA_NODE_STEP32(2)
     FRA_NODE_STEP32(3) FRA_NODE_STEP32(4) FRA_NODE_STEP32(5)
 #undef FRA_NODE_STEP32
-    wsync();
     if (lane >= 1 && p <= P && p <= pm) {
-      const int j = lane - (1 << p);
-      rice_pick32((uint32_t)((n >> p) - (j == 0 ? o : 0)), nd[lane], kn, bits32);
+      rice_pick32((uint32_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits32);
       big = kn > 14;
     }
-    if (P == 6 && pm == 6) {
+    if (P == 6 && pm == 6) {  // level 6: the finest sums at lane j
       uint32_t b6;
-      rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), nd[64 + lane], k6, b6);
+      rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), (uint32_t)Sv, k6, b6);
       tot6 = wave_sum32(b6);
       big6 = __any(k6 > 14);
     }
   } else {
     uint64_t S = Sv;
-    if (lane < (1 << P)) node[(1 << P) + lane] = S;
+    uint64_t nv = p == P ? bperm64(S, jn) : 0ull;
 #define FRA_NODE_STEP(S_)                                                          \
   if (P > S_) {                                                                    \
     S = up_add64<S_>(S);                                                           \
-    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
-      node[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = S;                          \
+    const uint64_t tv = bperm64(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
+    nv = p == P - S_ - 1 ? tv : nv;                                                \
   }
     FRA_NODE_STEP(0) FRA_NODE_STEP(1) FRA_NODE_STEP(2)
     FRA_NODE_STEP(3) FRA_NODE_STEP(4) FRA_NODE_STEP(5)
 #undef FRA_NODE_STEP
-    wsync();
     if (lane >= 1 && p <= P && p <= pm) {
-      const int j = lane - (1 << p);
       uint64_t bits;
-      rice_pick((uint64_t)((n >> p) - (j == 0 ? o : 0)), node[lane], kn, bits);
+      rice_pick((uint64_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits);
       bits32 = (uint32_t)bits;
       big = kn > 14;
     }
     if (P == 6 && pm == 6) {
       uint64_t b6;
-      rice_pick((uint64_t)((n >> 6) - (lane == 0 ? o : 0)), node[64 + lane], k6, b6);
+      rice_pick((uint64_t)((n >> 6) - (lane == 0 ? o : 0)), Sv, k6, b6);
       tot6 = wave_sum32((uint32_t)b6);
       big6 = __any(k6 > 14);
     }
@@ -327,7 +321,6 @@ __device__ __forceinline__ void porder_search_w(uint64_t Sv, unsigned long long*
   // partition j's parameter at order bp: node (bp, j) sits at lane 2^bp + j (level 6: k6 at lane j)
   const int kl = __shfl(kn, ((1 << (bp < 6 ? bp : 0)) + lane) & 63, 64);
   kreg = (uint32_t)(bp == 6 ? k6 : kl);
-  wsync();  // the node reads are done before the next search reuses the scratch
 }
 
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
@@ -459,13 +452,17 @@ __device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
 constexpr int kWPrefetch = 1024;
 
 template <int MAXLAG>
-__global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
+// occupancy target: 8 KiB of LDS lets 20 waves share a CU; <= 96 VGPRs make it 5 per SIMD
+#ifndef FRA_W_WAVES
+#define FRA_W_WAVES 5
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FRA_W_WAVES, 8)))
+k_analyze_w(JobArgs a, int src) {
   static_assert(MAXLAG == 8, "levels 3-6");
   __shared__ WaveSmem S;
   uint32_t* const sw = S.sw;
   const int lane = (int)threadIdx.x;
   FRA_WSTAMP(0)
-  const int bo = base_own(lane), bpv = base_prev(lane), bnx = base_next(lane);
   const int g = a.frame_base + (int)blockIdx.x;
   const int c = (int)blockIdx.y;
   const FrameDev fr = a.frames[g];
@@ -495,7 +492,6 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx) {
     const int32_t* lut = a.lut + (int64_t)fr.stream * a.lut_stride;
-    if (lane < 8) sw[lane] = 0u;  // zero chunk
     switch (src) {  // wave-uniform
       case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
       case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
@@ -525,10 +521,10 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
   auto shift_wasted = [&]() {  // samples >>= w (int16 pairs, arithmetic; the pad dwords too)
-    for (int k = lane; k < sdw(kWChunks, 0) - 8; k += 64) {
-      const uint32_t v = sw[8 + k];
+    for (int k = lane; k < (int)kBufWords; k += 64) {
+      const uint32_t v = sw[k];
       const uint32_t lo = (uint32_t)(lo16(v) >> w) & 0xFFFFu, hi = (uint32_t)(hi16(v) >> w);
-      sw[8 + k] = lo | (hi << 16);
+      sw[k] = lo | (hi << 16);
     }
   };
   if (w) shift_wasted();
@@ -540,13 +536,17 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   const int prec = qlp_precision(bps, n);
   const int lmax = cfg.max_lpc;                      // < n - 1
 
-  // ---- 3a. FIXED residual sums (3.8) by finite differences, per finest partition
-  uint32_t* const scr32 = reinterpret_cast<uint32_t*>(S.scr);
+  // ---- 3a. FIXED residual sums (3.8) by finite differences, per finest partition: group sums of the lanes
+  // of a partition, gathered so that lane p holds partition p (ds_bpermute from the group's last lane)
+  const int npl = 6 - gsl;  // log2 finest partitions per iteration
+  const int pj = lane >> npl;  // the iteration of partition `lane` (>= 4: lane >= 2^P, none)
+  const int psrc = ((lane & ((1 << npl) - 1)) << gsl) | ((1 << gsl) - 1);  // its group's last lane
+  uint32_t pfix[5] = {0, 0, 0, 0, 0};
   for (int j = 0; j < kWIters; j++) {
     const int t = 64 * j + lane;
     const bool head = t == 0;
     uint32_t D[14];
-    wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
+    wread_d14(sw, lane, j, D);
     int32_t x[28];
     unpack28(D, x);
 #pragma unroll
@@ -563,15 +563,10 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         s32 = sad_acc(ab, bb, s32);
       }
       // a partition of <= 512 samples: 2 sum |r| < 2^30
-      const uint32_t gs = group_sum32(s32, gsl);
-      if ((lane & ((1 << gsl) - 1)) == (1 << gsl) - 1) scr32[k * 64 + (t >> gsl)] = 2u * gs;
+      const uint32_t gs = bperm32(group_sum32(s32, gsl), psrc);
+      pfix[k] = pj == j ? 2u * gs : pfix[k];
     }
   }
-  wsync();
-  uint32_t pfix[5];
-#pragma unroll
-  for (int k = 0; k < 5; k++) pfix[k] = lane < (1 << P) ? scr32[k * 64 + lane] : 0u;
-  wsync();
   FRA_WSTAMP(2)
 
   // ---- running winner (FRA-1 3.8: first minimal estimate in model order)
@@ -607,13 +602,24 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       asm volatile("v_add_u32 %0, %0, %1" : "+v"(p2) : "v"(p3));
       asm volatile("v_add_u32 %0, %0, %1" : "+v"(p3) : "v"(p0));
     }
-    if ((p0 ^ p1 ^ p2 ^ p3) == 0x7FFFFFF3u) S.mdl[0][11] = 1;  // keep the chains alive
+    asm volatile("" ::"v"(p0 ^ p1 ^ p2 ^ p3));  // keep the chains alive
   }
 #endif
   FRA_WSTAMP(3)
   // ---- 3. LPC analysis per apodization window (3.4-3.7): lane 16 wi + o_l of window wi's lane group holds
   // that window's model (order o_l, quantised q, shift qsh, ok)
   int nlpc = 0;
+  // LPC model per window (levels 3-6: <= 3 windows): qlp coefficients, shift, order (0: none), usable
+  int32_t mq[kWinW][8], msh[kWinW], mo[kWinW];
+  bool mok[kWinW];
+#pragma unroll
+  for (int wi = 0; wi < kWinW; wi++) {
+    mo[wi] = 0;
+    mok[wi] = false;
+    msh[wi] = 0;
+#pragma unroll
+    for (int jx = 0; jx < 8; jx++) mq[wi][jx] = 0;
+  }
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
       nlpc = a.nwin;
@@ -630,21 +636,28 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         double s01[N16], s[N16];
 #pragma unroll
         for (int k = 0; k < N16; k++) { s01[k] = 0.0; s[k] = 0.0; }
+        // the lane's addresses are recomputed per window (opaque lane): hoisted out of the window loop
+        // they would stay live across it and cost registers the rest of the kernel needs
+        int lnw = lane;
+        asm volatile("" : "+v"(lnw));
         for (int j = 0; j < kWIters; j++) {
           double z[N16];
           // an iteration whose samples + look-ahead miss the window's nonzero extent sums exact zeros:
           // every chunk partial is +0.0 (k_analyze's inactive wave)
           if (lo < 1024 * j + 1024 + MAXLAG && hi > 1024 * j) {
-            const int t = 64 * j + lane, i0 = kChunk * t;
-            int32_t y[kChunk + MAXLAG];  // samples 16t .. 16t + 15 + MAXLAG (dword pairs: ds_read_b64)
+            const int t = 64 * j + lnw, i0 = kChunk * t;
+            // samples 16t .. 16t + 15 + MAXLAG: the chunk and the next one's first 8 (the last chunk's
+            // look-ahead re-reads itself: those samples meet 0.0f coefficients past n)
+            int32_t y[kChunk + MAXLAG];
+            {
+              const uint32_t* po = sw + 8 * lnw + kWIterDw * j;
+              const uint4 v0 = lds4(po), v1 = lds4(po + 4), v2 = lds4(t == kWChunks - 1 ? po : po + 8);
+              const uint32_t dw[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
 #pragma unroll
-            for (int p = 0; p < (kChunk + MAXLAG) / 4; p++) {
-              const uint32_t* src = sw + (p < kChunk / 4 ? bo : bnx) + kWIterDw * j + 2 * (p % (kChunk / 4));
-              const uint2 v = *reinterpret_cast<const uint2*>(src);
-              y[4 * p] = lo16(v.x);
-              y[4 * p + 1] = hi16(v.x);
-              y[4 * p + 2] = lo16(v.y);
-              y[4 * p + 3] = hi16(v.y);
+              for (int p = 0; p < (kChunk + MAXLAG) / 2; p++) {
+                y[2 * p] = lo16(dw[p]);
+                y[2 * p + 1] = hi16(dw[p]);
+              }
             }
             // coefficients exactly 1.0f inside the plateau: the product is the sample itself (no load, and
             // no multiply when the whole iteration lies inside); else loaded, entries at or past n 0.0f
@@ -725,14 +738,19 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       int qsh = 0;
       if (on) ok = quantize<MAXLAG>(lpo, lo, prec, q, qsh);
       const int o_l = nord > 0 ? (int)__builtin_ctz(rowbits | 0x10000u) : 0;
-      if (gon && lo == o_l) {  // the window's model (o_l = 0: none) to LDS for the candidate loop
+      // each window's model (lane 16 wi + o) to scalar registers for the candidate loop (o = 0: none)
 #pragma unroll
-        for (int jx = 0; jx < 8; jx++) S.mdl[gw][jx] = jx < MAXLAG ? q[jx < MAXLAG ? jx : 0] : 0;
-        S.mdl[gw][8] = qsh;
-        S.mdl[gw][9] = o_l;
-        S.mdl[gw][10] = ok ? 1 : 0;
+      for (int wi = 0; wi < kWinW; wi++) {
+        if (wi < nwin) {
+          const int ow = __builtin_amdgcn_readlane(o_l, 16 * wi);
+          const int L = 16 * wi + ow;
+          mo[wi] = ow;
+          mok[wi] = ow > 0 && __builtin_amdgcn_readlane((int)ok, L) != 0;
+          msh[wi] = __builtin_amdgcn_readlane(qsh, L);
+#pragma unroll
+          for (int jx = 0; jx < 8; jx++) mq[wi][jx] = __builtin_amdgcn_readlane(q[jx], L);
+        }
       }
-      wsync();
     }
   }
   FRA_WSTAMP(5)
@@ -743,37 +761,37 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
   // chunk's zig-zag residuals (int16 pairs), which the exact pass and the encoder then read instead of
   // recomputing the predictor twice (fallback: the samples are loaded again)
   int keep_wi = -1;
-  for (int wi = 0; wi < nlpc; wi++)
-    if (S.mdl[wi][9] != 0 && S.mdl[wi][10] != 0) keep_wi = wi;
-  keep_wi = __builtin_amdgcn_readfirstlane(keep_wi);
+#pragma unroll
+  for (int wi = 0; wi < kWinW; wi++)
+    if (mok[wi]) keep_wi = wi;
   bool kept_fit = false;
   uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
 #pragma unroll 1
   for (int ci = 0; ci < 2 + nlpc; ci++) {
     int m, o, sh = 0, type = 2;
     int32_t qm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t psum;
+    uint64_t psum = 0;
     if (ci < 2) {
       m = o = ci == 0 ? g1 : g2;
       psum = ci == 0 ? pf1 : pf2;
     } else {
       const int wi = ci - 2;
-      o = __builtin_amdgcn_readfirstlane(S.mdl[wi][9]);
-      if (o == 0 || !__builtin_amdgcn_readfirstlane(S.mdl[wi][10])) continue;  // no order / not quantisable
+      if (!(wi == 0 ? mok[0] : wi == 1 ? mok[1] : mok[2])) continue;  // no order / not quantisable
+      o = wi == 0 ? mo[0] : wi == 1 ? mo[1] : mo[2];
       m = 5 + wi;
       type = 3;
-      sh = __builtin_amdgcn_readfirstlane(S.mdl[wi][8]);
+      sh = wi == 0 ? msh[0] : wi == 1 ? msh[1] : msh[2];
 #pragma unroll
-      for (int jx = 0; jx < 8; jx++) qm[jx] = __builtin_amdgcn_readfirstlane(S.mdl[wi][jx]);
+      for (int jx = 0; jx < 8; jx++) qm[jx] = wi == 0 ? mq[0][jx] : wi == 1 ? mq[1][jx] : mq[2][jx];
       if (wi == keep_wi) {
         uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll 1
         for (int j = 0; j < kWIters; j++) {
           const int t = 64 * j + lane;
           const bool head = t == 0;
-          uint32_t* const po = sw + bo + kWIterDw * j;
+          uint32_t* const po = sw + 8 * lane + kWIterDw * j;
           uint32_t D[14];
-          wread_d14(po, sw + bpv + kWIterDw * j, D);
+          wread_d14(sw, lane, j, D);
           if (j > 0) {  // chunk 64 j - 1 already holds residuals: its last 12 samples came from lane 63
 #pragma unroll
             for (int k = 0; k < 6; k++) D[k] = lane == 0 ? carry[k] : D[k];
@@ -794,8 +812,8 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           wsync();  // (all lanes' sample reads of this iteration precede the stores)
 #pragma unroll
           for (int p = 0; p < kChunk / 4; p++) *reinterpret_cast<uint2*>(po + 2 * p) = make_uint2(pk[2 * p], pk[2 * p + 1]);
-          const uint64_t gs = group_sum_auto(2ull * acc, gsl);
-          if ((lane & ((1 << gsl) - 1)) == (1 << gsl) - 1) S.scr[t >> gsl] = gs;
+          const uint64_t gs = bperm64(group_sum_auto(2ull * acc, gsl), psrc);
+          psum = pj == j ? gs : psum;
         }
         kept_fit = !__any(um > 0xFFFFu);
       } else {
@@ -804,7 +822,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
           const int t = 64 * j + lane;
           const bool head = t == 0;
           uint32_t D[14];
-          wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
+          wread_d14(sw, lane, j, D);
           uint32_t acc = 0;
           switch (o) {
 #define FRA_CASE(O_) \
@@ -812,19 +830,16 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
             FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6) FRA_CASE(7) FRA_CASE(8)
 #undef FRA_CASE
           }
-          const uint64_t gs = group_sum_auto(2ull * acc, gsl);
-          if ((lane & ((1 << gsl) - 1)) == (1 << gsl) - 1) S.scr[t >> gsl] = gs;
+          const uint64_t gs = bperm64(group_sum_auto(2ull * acc, gsl), psrc);
+          psum = pj == j ? gs : psum;
         }
       }
-      wsync();
-      psum = lane < (1 << P) ? S.scr[lane] : 0ull;
-      wsync();
     }
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best;
     int bp;
     uint32_t kreg;
-    porder_search_w(psum, S.scr, P, pm, n, o, lane, best, bp, kreg);
+    porder_search_w(psum, P, pm, n, o, lane, best, bp, kreg);
     const uint64_t est = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + best;
     offer((uint32_t)est, m, type, o, sh, qm, bp, kreg);
   }
@@ -867,7 +882,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
     auto residuals = [&](int j, uint32_t (&un)[kChunk]) {
       const int t = 64 * j + lane;
       if (kept) {  // 8 dwords of int16 pairs
-        const uint32_t* po = sw + bo + kWIterDw * j;
+        const uint32_t* po = sw + 8 * lane + kWIterDw * j;
 #pragma unroll
         for (int p = 0; p < kChunk / 4; p++) {
           const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
@@ -879,7 +894,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
         return;
       }
       uint32_t D[14];
-      wread_d14(sw + bo + kWIterDw * j, sw + bpv + kWIterDw * j, D);
+      wread_d14(sw, lane, j, D);
       if (type == 3) {
 #pragma unroll
         for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
@@ -1040,7 +1055,7 @@ __global__ void __launch_bounds__(64, 4) k_analyze_w(JobArgs a, int src) {
       // residuals read before its words are zeroed and written: iteration j's last word + the spare one must
       // stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a compressible
       // rest -- the subframe goes to k_analyze)
-      bool ok = true;
+      bool ok = nw + 1 <= kBufWords;  // the whole subframe + the spare word fit the buffer
 #pragma unroll
       for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
       if (!ok) {

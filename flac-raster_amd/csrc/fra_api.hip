@@ -6,11 +6,10 @@
 // (graph-capturable).  Per-job launch sequence (fra_kernels.hip):
 //   k_norm_init, k_minmax, k_norm_finalize  (skipped when norm == 0)
 //   k_analyze  [frames x channels]
-//   k_frame_bytes + hipcub exclusive scan + k_group_offsets
+//   k_frame_scan (frame sizes + decoupled look-back scan; k_group_offsets after a previous group)
 //   k_assemble [frames]
 // Large plans run as FRA_GROUPS frame groups on their own streams (fra_plan_execute).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -34,7 +33,10 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, int32_t* redo,
                           unsigned* redo_count, int max_redo_blocks);
-hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s);
+int frame_scan_blocks(int nframes);
+hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
+                             unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
+                             unsigned tbase, unsigned tag, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
@@ -103,8 +105,13 @@ struct fra_plan {
   unsigned long long* d_foff = nullptr;
   uint8_t* d_out = nullptr;
   size_t out_cap = 0;
-  void* d_scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  // k_frame_scan look-back words and tickets per scan slot (frame group g: slot g; host bands and the
+  // timing pass: slot 0) and, on the host, each slot's ticket base and launch tag (launches on one slot
+  // are stream-ordered)
+  unsigned long long* d_look = nullptr;
+  unsigned* d_ticket = nullptr;
+  int look_stride = 0;
+  std::vector<unsigned> scan_tbase, scan_tag;
   uint16_t* d_crctab = nullptr;
   uint32_t* d_tmp = nullptr;
   uint32_t* d_fmeta = nullptr;
@@ -119,7 +126,6 @@ struct fra_plan {
   std::vector<hipStream_t> aux;
   std::vector<hipEvent_t> gev;          // [0] start, then per group: offsets-published, done
   unsigned long long* d_gbase = nullptr;  // [max(groups, host bands) + 1] byte offset of each group's first frame
-  size_t scan_stride = 0;               // bytes of scan workspace per group
   // host pipeline (fra_plan_encode_host): row bands of windows; band b copies raster rows [r0, r1)
   // before its kernels run (rows already copied by earlier bands are not copied again)
   struct HBand { Group g; int64_t r0, r1; };
@@ -158,6 +164,14 @@ struct fra_plan {
   hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
   bool ana_pending[2] = {false, false};
   bool raster_dirty = false;  // a host raster copy on the plan's stream the norm stream must wait for
+  // Infinity-Cache chunking of a pipelined execute (FRA_CHUNK_MB): the single group split into chunks of
+  // about that many raster bytes; chunk i's norm stage waits for chunk i-2's analysis (cev ring, counted
+  // across executes by chunk_seq), so it runs under chunk i-1's analysis and leaves chunk i's rows in the
+  // 256 MB Infinity Cache for chunk i's analysis; each chunk's frame scan + assembly follow on the pack
+  // stream while its slots are still cache-resident
+  std::vector<Group> chunks;
+  hipEvent_t cev[4] = {};
+  uint64_t chunk_seq = 0;
   bool resync = false;        // serial work was queued on the plan's stream since the last pipelined execute
   // timing
   bool timing = false;
@@ -337,12 +351,16 @@ void fra_plan_destroy(fra_plan* p) {
     if (p->ev_norm[b]) (void)hipEventDestroy(p->ev_norm[b]);
     if (p->ev_ana[b]) (void)hipEventDestroy(p->ev_ana[b]);
   }
+  for (auto e : p->cev) {
+    if (e) (void)hipEventDestroy(e);
+  }
   if (p->ev_raster) (void)hipEventDestroy(p->ev_raster);
   (void)hipFree(p->d_sf);
   (void)hipFree(p->d_fbytes);
   (void)hipFree(p->d_foff);
   (void)hipFree(p->d_out);
-  (void)hipFree(p->d_scan_tmp);
+  (void)hipFree(p->d_look);
+  (void)hipFree(p->d_ticket);
   (void)hipFree(p->d_crctab);
   (void)hipFree(p->d_tmp);
   (void)hipFree(p->d_fmeta);
@@ -431,7 +449,7 @@ static int plan_build(fra_plan* p) {
   else bps = (j.dtype == FRA_I16 || j.dtype == FRA_U8 || j.dtype == FRA_I8) ? 16 : 32;
   p->b32 = bps == 32;
   // FRA-1 3.1b mid-side for 2-channel 16-bps streams at the levels whose libFLAC preset enables it:
-  // four virtual channels (L, R, M, S) are analysed per frame, k_frame_bytes keeps the cheapest pair
+  // four virtual channels (L, R, M, S) are analysed per frame, k_frame_scan keeps the cheapest pair
   const bool ms = j.channels == 2 && bps == 16 && level_cfg(j.level).ms;
   p->cmax = ms ? 4 : j.channels;
   const int sbps_max = ms ? bps + 1 : bps;  // side samples carry one more bit
@@ -610,19 +628,15 @@ static int plan_build(fra_plan* p) {
     p->groups.back().w1 = (int)p->streams.size();
     p->groups.back().f1 = nfr;
     build_host_bands(p, nfr);
-    size_t mx = 0, tb = 0;
-    std::vector<fra_plan::Group> scan_shapes(p->groups);
-    for (const auto& hb : p->hbands) scan_shapes.push_back(hb.g);
-    for (const auto& gr : scan_shapes) {
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->d_fbytes, p->d_foff, std::max(1, gr.f1 - gr.f0),
-                                              p->ctx->stream));
-      mx = std::max(mx, tb);
-    }
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->d_fbytes, p->d_foff, std::max(1, nfr), p->ctx->stream));
-    mx = std::max(mx, tb);
-    p->scan_stride = (std::max<size_t>(16, mx) + 255) & ~(size_t)255;
-    p->scan_tmp_bytes = p->scan_stride * p->groups.size();
-    HIPCHK(hipMalloc(&p->d_scan_tmp, p->scan_tmp_bytes));
+    // look-back words (zero: no tag yet) and tickets of every scan slot, sized for the whole plan
+    const int nslot = (int)p->groups.size();
+    p->look_stride = std::max(1, frame_scan_blocks(nfr));
+    HIPCHK(hipMalloc(&p->d_look, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
+    HIPCHK(hipMemset(p->d_look, 0, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
+    HIPCHK(hipMalloc(&p->d_ticket, sizeof(unsigned) * nslot));
+    HIPCHK(hipMemset(p->d_ticket, 0, sizeof(unsigned) * nslot));
+    p->scan_tbase.assign(nslot, 0u);
+    p->scan_tag.assign(nslot, 0u);
     HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) * (std::max(p->groups.size(), p->hbands.size()) + 1)));
     for (size_t g = 1; g < p->groups.size(); g++) {
       hipStream_t st = nullptr;
@@ -722,6 +736,34 @@ static int plan_build(fra_plan* p) {
         // start takes the slots the background assembly was using) (r03 v14)
         if (!p->b32)
           for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
+      }
+      {  // Infinity-Cache chunks (windows in order, about FRA_CHUNK_MB of raster each)
+        const char* cm = getenv("FRA_CHUNK_MB");
+        const double mb = cm ? atof(cm) : 0.0;
+        const double fbytes = (double)j.blocksize * std::max(1, j.channels) * elem_size(j.dtype);
+        const int64_t per = mb > 0 ? std::max<int64_t>(1, (int64_t)(mb * 1048576.0 / fbytes)) : (int64_t)nfr;
+        const int nc = (int)std::min<int64_t>(64, (nfr + per - 1) / per);
+        if (nc > 1) {
+          int w = 0, f = 0;
+          for (int c = 0; c < nc && w < (int)p->streams.size(); c++) {
+            const int64_t target = (int64_t)nfr * (c + 1) / nc;
+            fra_plan::Group gr{w, w, f, f};
+            while (w < (int)p->streams.size() && (c == nc - 1 || f < target || gr.f1 == gr.f0)) {
+              f += p->streams[w].nframes;
+              w++;
+              gr.w1 = w;
+              gr.f1 = f;
+            }
+            p->chunks.push_back(gr);
+          }
+          p->chunks.back().w1 = (int)p->streams.size();
+          p->chunks.back().f1 = nfr;
+          // byte offsets of every chunk's first frame (gbase[c]; the chunks scan in order on the pack stream)
+          (void)hipFree(p->d_gbase);
+          HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) *
+                                            (std::max({p->groups.size(), p->hbands.size(), p->chunks.size()}) + 1)));
+          for (auto& e : p->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
       }
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
@@ -905,7 +947,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
-  // pipelined execute: the frame-size chain (k_frame_bytes, scan, k_group_offsets) only feeds this
+  // pipelined execute: the frame-size chain (k_frame_scan) only feeds this
   // execute's assembly, so it goes onto the pack stream with it and the plan's stream proceeds straight to
   // the next execute's analysis
   // background form of k_assemble (<= 32 VGPRs, ~one workgroup per CU) beside the next execute's analysis
@@ -916,15 +958,20 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     st = pack_st;
     pack_st = nullptr;
   }
-  HIPCHK(launch_frame_bytes(ga, st));
+  // frame sizes and offsets: one k_frame_scan; with the group's base already ordered (first / only group,
+  // host bands on one stream) it writes the final offsets itself, else k_group_offsets adds the base once
+  // the previous group has published it
   if (nf > 0) {
-    size_t tb = p->scan_stride;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum((uint8_t*)p->d_scan_tmp + (size_t)(slot < 0 ? gi : slot) * p->scan_stride, tb,
-                                            p->d_fbytes + gr.f0, p->d_foff + gr.f0, nf, st));
+    const int sl = slot < 0 ? gi : slot;
+    const unsigned tag = ++p->scan_tag[sl];
+    HIPCHK(launch_frame_scan(ga, p->d_gbase, gi, gi == ng - 1, ev_prev ? 0 : 1, host_mirror,
+                             p->d_look + (size_t)sl * p->look_stride, p->d_ticket + sl, p->scan_tbase[sl], tag, st));
+    p->scan_tbase[sl] += (unsigned)frame_scan_blocks(nf);
   }
   if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
-  HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
-                              a.nframes_total, st, host_mirror));
+  if (nf == 0 || ev_prev)
+    HIPCHK(launch_group_offsets(p->d_foff, p->d_fbytes, p->d_gbase, gi, gr.f0, nf, gi == ng - 1,
+                                a.nframes_total, st, host_mirror));
   if (ev_pub) HIPCHK(hipEventRecord(ev_pub, st));
   if (t_scan) HIPCHK(hipEventRecord(t_scan, st));
   if (pack_st) {  // assembly on the pack stream once this group's offsets exist
@@ -968,9 +1015,21 @@ int fra_plan_execute(fra_plan* p) {
       HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_raster, 0));
       p->raster_dirty = false;
     }
-    rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
-                   p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
-    if (rc) return rc;
+    if (p->chunks.empty()) {
+      rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
+                     p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
+      if (rc) return rc;
+    } else {
+      const int nc = (int)p->chunks.size();
+      for (int c = 0; c < nc; c++, p->chunk_seq++) {
+        // chunk i's norm stage after chunk i-2's analysis: one chunk ahead of the analysis, not more
+        if (p->chunk_seq >= 2) HIPCHK(hipStreamWaitEvent(p->nstream, p->cev[(p->chunk_seq - 2) & 3], 0));
+        rc = run_group(p, p->chunks[c], c, nc, as, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, p->pack,
+                       p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(p->cev[p->chunk_seq & 3], as));  // (nothing after the analysis on `as`)
+      }
+    }
     p->ana_pending[b] = true;
     HIPCHK(hipEventRecord(p->ev_pack[b], p->pack));
     p->pack_pending[b] = true;
@@ -1094,7 +1153,7 @@ int fra_plan_timing(fra_plan* p, float* ms4, int32_t* n) {
 int fra_plan_set_first_frame(fra_plan* p, int32_t first_frame) {
   if (!p || first_frame < 0) return set_err(FRA_E_INVALID, "bad argument");
   (void)hipSetDevice(p->ctx->device);
-  // pipelined executes still in flight read frame_number0 on the analysis / pack streams (k_frame_bytes):
+  // pipelined executes still in flight read frame_number0 on the analysis / pack streams (k_frame_scan):
   // let them finish before the table changes under them
   if (int rc = plan_sync_all(p)) return rc;
   p->job.first_frame = first_frame;

@@ -9,7 +9,7 @@
 //
 // Gather formulation: every thread builds whole output quads (4 dwords, 16-byte aligned in the
 // output).  Global dword G0+k (G0 = (F-A)/4, A = F & 3) holds frame bits [8(4k-A), +32): the header
-// and the channel blobs are laid end to end at known bit offsets (k_frame_bytes), so a quad that lies
+// and the channel blobs are laid end to end at known bit offsets (k_frame_scan), so a quad that lies
 // inside one blob is a funnel shift (one shift for all four) of 5 consecutive slot words: one 16-byte
 // load + one dword load + one 16-byte store.  Quads touching the header, a blob boundary or the frame
 // ends resolve dword by dword; the first/last dwords (shared with the neighbouring frames) get byte
@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t gf16_mul_dev(uint32_t a, uint32_t b) {
 struct alignas(16) AssembleSmem {
   uint16_t T[16][256];  // slice-by-16: T[k][v] = CRC of v followed by k zero bytes
   uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..10 (tree 4..9, Horner 10)
-  uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_bytes); [wave]
+  uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_scan); [wave]
   uint32_t tailw[4];    // the output window of the last, partial dword (bytes [4*NF - A, L)); [wave]
 };
 // background form: only the per-quad tables in LDS (9.3 KiB: it fits beside four 32-bps k_analyze
@@ -102,7 +102,7 @@ __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
 
 // one frame by one wave (four frames per workgroup, no workgroup barrier per frame, the CRC tables copied
 // to LDS once for the four by the caller), U quads per lane per round.  Header and blob bounds come
-// precomputed from k_frame_bytes, so every metadata load is issued in the first round
+// precomputed by k_frame_scan, so every metadata load is issued in the first round
 template <int U, typename SM>
 __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM& S) {
   constexpr int NT = 64;  // lanes per frame
@@ -146,7 +146,7 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   const int pad = (int)((NT - (NQ % NT)) % NT);
   const int kfull = A == 0 ? 0 : 1;        // first dword written whole
   const uint32_t* slots = a.tmp + (size_t)g * a.cmax * a.tmp_stride;
-  // slot of output channels 0 / 1 (k_frame_bytes: identity unless a mid-side assignment was chosen)
+  // slot of output channels 0 / 1 (k_frame_scan: identity unless a mid-side assignment was chosen)
   const uint32_t smap = C == 2 ? (uint32_t)__builtin_amdgcn_readfirstlane(gmeta[kHdrWords - 1]) : 0u;
   auto vslot = [&](int oc) -> int { return C == 2 ? (int)((smap >> (8 * oc)) & 0xFFu) : oc; };
 #ifdef FRA_GUARD

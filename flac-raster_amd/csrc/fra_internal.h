@@ -154,7 +154,7 @@ struct NormDev {       // per stream, filled on device
   double mn, mx, range;             // normalize_to_audio parameters (normalization.py:148-159)
 };
 
-// One analysed subframe (FRA-1 decision), written by k_analyze, read by k_frame_bytes/k_pack.
+// One analysed subframe (FRA-1 decision), written by k_analyze, read by k_frame_scan / k_assemble.
 struct SfDesc {
   uint32_t bits;      // exact subframe size in bits
   uint8_t type;       // 0 CONSTANT, 1 VERBATIM, 2 FIXED, 3 LPC
@@ -170,7 +170,7 @@ struct SfDesc {
   uint8_t k[kMaxPart];
 };
 
-// per-frame metadata written by k_frame_bytes for k_assemble: words [0, kHdrWords) = frame header and
+// per-frame metadata written by k_frame_scan for k_assemble: words [0, kHdrWords) = frame header and
 // its CRC-8 as big-endian words (zero padded), words [kHdrWords, +kMaxChannels+2) = bit bounds:
 // 0, header bits, end of channel 0, ..., end of channel C-1 (unused entries = 0xFFFFFFFF)
 // CRC-16 table layout (fra_api.hip crc16_tables): [0, 1024) slice-by-4 byte tables, [1024, +24*512)
@@ -207,7 +207,7 @@ struct JobArgs {
   int32_t vec8;            // k_analyze may load 8-byte sample vectors (host-checked alignment)
   int32_t off32;           // every frame's samples of one channel lie within 2^31 bytes of its first row
                            // (k_analyze fast load path: 32-bit lane offsets from a uniform base)
-  int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_bytes / k_assemble):
+  int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_scan / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
   int32_t* redo;           // k_analyze_w appends (frame * 8 + channel) of the subframes it leaves to k_analyze;
   unsigned* redo_count;    //   k_analyze with redo set works through the list (null: the normal grid)

@@ -12,7 +12,7 @@
 //   k_minmax      per (row segment, stream): nanmin/nanmax over all bands of the window (a3)
 //   k_analyze     per (frame, channel) = subframe: normalise, wasted bits, windows,
 //                 autocorrelation, Levinson-Durbin, qlp, model search, exact Rice bits -> SfDesc
-//   k_frame_bytes per frame: header + subframe bits + pad + CRC-16 -> bytes
+//   k_frame_scan per frame group: header + subframe bits + pad + CRC-16 -> bytes -> byte offsets
 //   (hipcub exclusive scan of frame bytes -> frame byte offsets)
 //   k_pack        per frame: re-read + re-normalise, residual of the chosen model, bit-pack into
 //                 an LDS bit buffer, flush to HBM at the frame's byte offset, CRC-8/CRC-16
@@ -173,13 +173,11 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
   }
 }
 
-__global__ void k_frame_bytes(JobArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.frame_count) return;
-  const int g = a.frame_base + i;
+// One frame's header (+ CRC-8) and blob bit bounds -> fmeta, its byte size -> frame_bytes; returns the size.
+// FRA-1 3.1b: a mid-side stream keeps the first minimum of L+R, L+S, S+R, M+S (virtual channels 0..3)
+__device__ uint64_t frame_bytes_one(const JobArgs& a, int g) {
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
-  // FRA-1 3.1b: a mid-side stream keeps the first minimum of L+R, L+S, S+R, M+S (virtual channels 0..3)
   int chan_code = st.channels - 1, va = 0, vb = 1;
   if (st.ms) {
     const SfDesc* sd = a.sf + (size_t)g * a.cmax;
@@ -216,7 +214,98 @@ __global__ void k_frame_bytes(JobArgs a) {
     if (c < st.channels) bits += a.sf[(size_t)g * a.cmax + vc].bits;
     m[kHdrWords + 2 + c] = c < st.channels ? bits : 0xFFFFFFFFu;
   }
-  a.frame_bytes[g] = ((uint64_t)(bits + 7) >> 3) + 2;
+  const uint64_t fb = ((uint64_t)(bits + 7) >> 3) + 2;
+  a.frame_bytes[g] = fb;
+  return fb;
+}
+
+// Frame sizes -> byte offsets of a frame group in ONE launch (replaces k_frame_bytes + a library exclusive
+// scan + k_group_offsets: two to three fewer dependent launches per execute): every workgroup sizes 1,024
+// frames (4 per thread), then a single-pass scan with decoupled look-back (Merrill & Garland) over
+// workgroups in TICKET order -- a workgroup only ever waits on workgroups that took an earlier ticket, so
+// are already running: no assumption on dispatch order or co-residency.  Look-back words: [63:42] launch tag,
+// [41:40] flag (1 aggregate, 2 inclusive prefix), [39:0] bytes (< 1 TiB per group); the tag makes clearing them unnecessary.
+// add_base: the group's base offset gbase[grp] is ordered before this launch -> final offsets, gbase[grp+1]
+// (+ frame_off[nframes] for the last group, + the host mirror); else group-relative offsets (k_group_offsets
+// adds the base once the previous group is done).
+constexpr int kScanItems = 4;
+constexpr int kScanBlock = 256 * kScanItems;
+constexpr uint64_t kScanValMask = (1ull << 40) - 1;
+__global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long long* gbase, int grp, int last,
+                                                    int add_base, unsigned long long* host_mirror,
+                                                    unsigned long long* look, unsigned* ticket, unsigned tbase,
+                                                    unsigned tag) {
+  __shared__ unsigned s_t;
+  __shared__ uint64_t s_w[4];
+  __shared__ uint64_t s_excl;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_t = atomicAdd(ticket, 1u) - tbase;
+  __syncthreads();
+  const int t = (int)s_t;  // this workgroup's position in the scan
+  const int n = a.frame_count;
+  uint64_t fb[kScanItems];
+  uint64_t loc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    const int i = t * kScanBlock + tid * kScanItems + k;
+    fb[k] = i < n ? frame_bytes_one(a, a.frame_base + i) : 0ull;
+    loc += fb[k];
+  }
+  // workgroup-inclusive scan of the per-thread sums: wave scan by DPP-free shuffles, then the 4 wave totals
+  uint64_t incl = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) s_w[wv] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    wbase += k < wv ? s_w[k] : 0ull;
+    agg += s_w[k];
+  }
+  if (tid == 0) {
+    const uint64_t tg = (uint64_t)(tag & 0x3FFFFFu) << 42;
+    uint64_t excl = 0;
+    if (t == 0) {
+      __hip_atomic_store(&look[0], tg | (2ull << 40) | (agg & kScanValMask), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&look[t], tg | (1ull << 40) | (agg & kScanValMask), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = t - 1; j >= 0;) {
+        const uint64_t w = __hip_atomic_load(&look[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t fl = (uint32_t)(w >> 40) & 3u;
+        if ((w & ~((1ull << 42) - 1)) != tg || fl == 0) {
+          __builtin_amdgcn_s_sleep(1);  // workgroup j (an earlier ticket, so running) has not published yet
+          continue;
+        }
+        excl += w & kScanValMask;
+        if (fl == 2) break;
+        j--;
+      }
+      __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_excl = excl;
+  }
+  __syncthreads();
+  const uint64_t base = add_base && grp > 0 ? gbase[grp] : 0ull;
+  uint64_t off = base + s_excl + wbase + incl - loc;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    const int i = t * kScanBlock + tid * kScanItems + k;
+    if (i < n) a.frame_off[a.frame_base + i] = off;
+    off += fb[k];
+    if (add_base && i == n - 1) {  // the group's end
+      gbase[grp + 1] = off;
+      if (last) a.frame_off[a.nframes_total] = off;
+      if (host_mirror) {  // page-locked host copy for the host pipeline (no copy-engine command needed)
+        host_mirror[grp + 1] = off;
+        __threadfence_system();
+      }
+    }
+  }
 }
 
 // ============================================================================ launchers
@@ -296,8 +385,13 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
   return hipGetLastError();
 }
 
-hipError_t launch_frame_bytes(const JobArgs& a, hipStream_t s) {
-  if (a.frame_count > 0) k_frame_bytes<<<(a.frame_count + 255) / 256, 256, 0, s>>>(a);
+int frame_scan_blocks(int nframes) { return (nframes + kScanBlock - 1) / kScanBlock; }
+hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
+                             unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
+                             unsigned tbase, unsigned tag, hipStream_t s) {
+  if (a.frame_count > 0)
+    k_frame_scan<<<frame_scan_blocks(a.frame_count), 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look,
+                                                                  ticket, tbase, tag);
   return hipGetLastError();
 }
 

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Same-box A/B of the pipelined step: ab_step.py <config> <lib.so|-> [NAME=VALUE ...]
+
+Environment assignments are applied before the plan is created (FRA_CHUNK_MB, FRA_ANALYZE_WG, ...).
+Prints the serial per-kernel times (timing mode, 5 executes) and the pipelined step time (median of
+5 runs of 20 back-to-back executes, wall clock around a sync), plus the output size as a bytes check."""
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "flac-raster_amd"))
+sys.path.insert(0, str(ROOT))
+import numpy as np  # noqa: E402
+
+from flac_raster import _native as N  # noqa: E402
+
+cfgname = sys.argv[1] if len(sys.argv) > 1 else "c4"
+if len(sys.argv) > 2 and sys.argv[2] != "-":
+    N._LIB_PATH = Path(sys.argv[2]).resolve()
+envs = [a for a in sys.argv[3:] if "=" in a]
+for kv in envs:
+    k, v = kv.split("=", 1)
+    os.environ[k] = v
+import bench  # noqa: E402
+
+cfg = dict(bench.CONFIGS[cfgname])
+ctx = N.Context(0)
+B, H, W = cfg["bands"], cfg["H"], cfg["W"]
+dt = np.dtype(cfg["dtype"])
+dev = ctx.alloc(B * H * W * dt.itemsize)
+ctx.synth(cfg["kind"], bench.SEED, B, H, W, dev)
+wins = bench.tiles(H, W, cfg["tile"])
+plan = N.Plan(ctx, dev, True, dt, B, (H * W, W, 1), wins, cfg["level"], 4096, cfg["norm"])
+plan.execute(); plan.sync()
+plan.enable_timing(True)
+for _ in range(5):
+    plan.execute()
+plan.sync()
+ms, n = plan.timing()
+plan.enable_timing(False)
+K = 20 if cfgname != "c5" else 4
+steps = []
+for _ in range(5):
+    plan.execute(); plan.execute(); plan.sync()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        plan.execute()
+    plan.sync()
+    steps.append((time.perf_counter() - t0) * 1e3 / K)
+_, total = plan.result()
+print(f"{N._LIB_PATH.name:34s} {' '.join(envs) or '-':22s} analyze {ms[1]/n:7.3f}  scan {ms[2]/n:6.3f}  "
+      f"pack {ms[3]/n:6.3f}  step {np.median(steps):7.3f} ms (min {min(steps):.3f})  out {total}", flush=True)
