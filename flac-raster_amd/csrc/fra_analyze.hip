@@ -1478,10 +1478,9 @@ template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   if (a.redo) {
-    // redo-list mode (after k_analyze_w): the subframes it handed back, entry = frame * 8 + channel, by a
-    // grid of workgroups striding over the list
-    const int cnt = (int)__builtin_amdgcn_readfirstlane((int)*a.redo_count);
-    for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
+    // list mode (beside k_analyze_w): the partial subframes, entry = frame * 8 + channel, by a grid of
+    // workgroups striding over the list
+    for (int i = (int)blockIdx.x; i < a.redo_n; i += (int)gridDim.x) {
       __syncthreads();  // the previous entry's LDS is dead
       const int e = __builtin_amdgcn_readfirstlane(a.redo[i]);
       analyze_wg<B32, MAXLAG>(a, src, e >> 3, e & 7, i & 3, false, S);
@@ -1509,25 +1508,35 @@ namespace fra {
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s);
 
 // wave: 16-bit plans whose full frames k_analyze_w takes (fra_api.hip wave_path): k_analyze_w over the launch's
-// frames, handing partial frames and the subframes it does not finish (winner not its kept LPC model, VERBATIM,
-// an encode that would overrun its samples) to a redo list that k_analyze then works through; redo / redo_count
-// are the list and its counter (zeroed here first), capacity frames x channels
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, int32_t* redo,
-                          unsigned* redo_count, int max_redo_blocks) {
+// frames, k_analyze over `part` (the launch's npart partial subframes, frame * 8 + channel), both complete
+// (side, ev_fork, ev_join: the partial subframes run on the side stream beside k_analyze_w -- a handful of
+// workgroups that would otherwise idle the device for their whole latency after it -- joined back before the
+// caller's next work on s; null side: after k_analyze_w on s)
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, const int32_t* part,
+                          int npart, int max_part_blocks, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (a.frame_count <= 0) return hipSuccess;
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
   if (wave && !b32 && ml == 8) {
     const int cw = ms ? 2 : a.cmax;
-    hipError_t e = hipMemsetAsync(redo_count, 0, sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
-    JobArgs wa = a;
-    wa.redo = redo;
-    wa.redo_count = redo_count;
-    if ((e = launch_analyze_w(src, a.level, wa, cw, s)) != hipSuccess) return e;
-    const int cap = a.frame_count * cw;
-    k_analyze<false, 8><<<(unsigned)std::min(cap, max_redo_blocks), kThreads, 0, s>>>(wa, src);
+    hipError_t e = hipSuccess;
+    auto partial = [&](hipStream_t ps) {
+      JobArgs wa = a;
+      wa.redo = part;
+      wa.redo_n = npart;
+      k_analyze<false, 8><<<(unsigned)std::min(npart, max_part_blocks), kThreads, 0, ps>>>(wa, src);
+    };
+    const bool fork = npart > 0 && side;
+    if (fork) {
+      if ((e = hipEventRecord(ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, ev_fork, 0)) != hipSuccess)
+        return e;
+      partial(side);
+      if ((e = hipEventRecord(ev_join, side)) != hipSuccess) return e;
+    }
+    if ((e = launch_analyze_w(src, a.level, a, cw, s)) != hipSuccess) return e;
+    if (fork && (e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return e;
+    if (npart > 0 && !side) partial(s);
     if (ms) {
       grid.y = 2;
       k_analyze<true, 8><<<grid, kThreads, 0, s>>>(a, src);

@@ -9,8 +9,8 @@
 // Scope: full 4096-sample frames of a <= 16-bit integer raster whose normalisation goes through the
 // per-tile table (k_norm_lut), 8-byte sample vectors, levels 0-6 (lag <= 8, <= 3 apodization windows):
 // the C3/C4 workloads.  Everything else (partial last frames, raw int16 input, levels 7-8, 32-bps and
-// the mid-side virtual channels) stays on k_analyze; the launcher routes the partial frames there
-// through a frame list.
+// the mid-side virtual channels) stays on k_analyze; the launcher runs it over the plan's list of partial
+// subframes (known at plan creation), so this kernel finishes every subframe it starts.
 //
 // Why a wave and not a workgroup: k_analyze's 256-thread workgroup spends 43 % of its wave cycles
 // parked at s_waitcnt / s_barrier -- eight barriers per subframe, Levinson-Durbin on 16
@@ -36,7 +36,7 @@ constexpr int kWChunks = kMaxBlock / kChunk;  // 256
 constexpr int kWIters = kWChunks / 64;        // chunks per lane
 
 // LDS per wave: exactly the 4,096 int16 samples (8 KiB: 20 waves per CU), chunk t (16 samples) at dwords
-// [8t, 8t + 8).  The bit buffer aliases them (<= 2,047 words + one spare; a longer subframe goes to the redo list)
+// [8t, 8t + 8).  The bit buffer aliases them (<= 2,047 words + one spare; a longer subframe takes the sample path)
 struct WaveSmem {
   uint32_t sw[8 * kWChunks];
 };
@@ -249,7 +249,10 @@ __device__ __forceinline__ void porder_search_w(uint64_t Sv, int P, int pm, int 
   int k6 = 0;
   if (__all(Sv < (1ull << 23))) {  // every node sum < 2^29: 32-bit arithmetic (rice_pick32), bit-identical
     uint32_t S = (uint32_t)Sv;
-    uint32_t nv = p == P ? bperm32(S, jn) : 0u;  // level P <= 5: the finest sums themselves
+    // level P <= 5: the finest sums themselves (every ds_bpermute runs on all 64 lanes: a source lane outside
+    // EXEC would read as 0, so none may sit under a lane-dependent condition)
+    const uint32_t fin = bperm32(S, jn & 63);
+    uint32_t nv = p == P ? fin : 0u;
 #define FRA_NODE_STEP32(S_)                                                        \
   if (P > S_) {                                                                    \
     S = up_add32<S_>(S);                                                           \
@@ -271,7 +274,8 @@ __device__ __forceinline__ void porder_search_w(uint64_t Sv, int P, int pm, int 
     }
   } else {
     uint64_t S = Sv;
-    uint64_t nv = p == P ? bperm64(S, jn) : 0ull;
+    const uint64_t fin = bperm64(S, jn & 63);
+    uint64_t nv = p == P ? fin : 0ull;
 #define FRA_NODE_STEP(S_)                                                          \
   if (P > S_) {                                                                    \
     S = up_add64<S_>(S);                                                           \
@@ -323,13 +327,45 @@ __device__ __forceinline__ void porder_search_w(uint64_t Sv, int P, int pm, int 
   kreg = (uint32_t)(bp == 6 ? k6 : kl);
 }
 
+#ifdef FRA_STAMPS
+// diagnostic build only (csrc/Makefile `wstamps`, tools/wstamp_phases.py): lane 0 of the first kWStampW waves
+// stores s_memtime after each phase, inside the real steady state
+constexpr unsigned kWStampW = 1u << 18, kWStampN = 16;
+__device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
+#define FRA_WSTAMP(k)                                                                            \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = __builtin_amdgcn_s_memtime();      \
+  }
+#define FRA_WSTAMP_VAL(k, v)                                                                     \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = (unsigned long long)(v);            \
+  }
+// FRA_WSTAMP_FINE: the load phase split at forced waits (metadata, raw rows, LUT gathers + LDS stores)
+#ifdef FRA_WSTAMP_FINE
+#define FRA_WSTAMP_WAIT(k)                                      \
+  {                                                             \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    FRA_WSTAMP(k)                                               \
+  }
+#endif
+#endif
+#ifndef FRA_WSTAMP
+#define FRA_WSTAMP(k)
+#define FRA_WSTAMP_VAL(k, v)
+#endif
+#ifndef FRA_WSTAMP_WAIT
+#define FRA_WSTAMP_WAIT(k) {}
+#endif
+
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
 // lane l loads the 8-byte vectors l + 64k (all issued before the first use), gathers each sample's audio
 // value from the tile's table, packs int16 pairs and stores 4 samples per ds_write_b64
 template <int SRC>
 __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st, const FrameDev& fr, int c,
                                           const int32_t* lut, uint32_t* sw, int lane, uint32_t& orv, int32_t& vmin,
-                                          int32_t& vmax) {
+                                          int32_t& vmax, bool stamp) {
   using T = typename RawType<SRC>::T;
   constexpr int V = 8 / (int)sizeof(T);
   constexpr int NV = kMaxBlock / 64 / V;
@@ -359,6 +395,7 @@ __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st,
       }
     }
   }
+  if (stamp) FRA_WSTAMP_WAIT(11)
   uint32_t orp = 0;
   i16x2 pmin = {32767, 32767}, pmax = {-32768, -32768};
 #pragma unroll
@@ -382,6 +419,7 @@ __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st,
   orv |= (orp | (orp >> 16)) & 0xFFFFu;
   vmin = min(vmin, min((int32_t)pmin.x, (int32_t)pmin.y));
   vmax = max(vmax, max((int32_t)pmax.x, (int32_t)pmax.y));
+  if (stamp) FRA_WSTAMP_WAIT(12)
 }
 
 // 16-bit path: sum of |LPC residual| of order O over one chunk (lpc_abs16_raw without the kept residuals),
@@ -427,25 +465,6 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
 
 }  // namespace
 
-#ifdef FRA_STAMPS
-// diagnostic build only (csrc/Makefile `wstamps`, tools/wstamp_phases.py): lane 0 of the first kWStampW waves
-// stores s_memtime after each phase, inside the real steady state
-constexpr unsigned kWStampW = 1u << 18, kWStampN = 10;
-__device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
-#define FRA_WSTAMP(k)                                                                            \
-  if (lane == 0) {                                                                               \
-    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
-    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = __builtin_amdgcn_s_memtime();      \
-  }
-#define FRA_WSTAMP_VAL(k, v)                                                                     \
-  if (lane == 0) {                                                                               \
-    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
-    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = (unsigned long long)(v);            \
-  }
-#else
-#define FRA_WSTAMP(k)
-#define FRA_WSTAMP_VAL(k, v)
-#endif
 
 // prefetch distance in waves: ~a quarter of the 4,096 waves resident chip-wide (16 per CU), so the rows are
 // in L2 (1 MiB of rows per XCD in flight) when that wave starts
@@ -468,15 +487,8 @@ k_analyze_w(JobArgs a, int src) {
   const FrameDev fr = a.frames[g];
   const StreamDev st = a.streams[fr.stream];
   if (c >= (st.ms ? 2 : st.channels)) return;
-  // a subframe this kernel does not finish: appended to the redo list that k_analyze works through next
-  auto hand_back = [&](int why) {
-    FRA_WSTAMP_VAL(9, why)
-    if (lane == 0) a.redo[atomicAdd(a.redo_count, 1u)] = g * 8 + c;
-  };
-  if (fr.n != kMaxBlock) {  // partial last frames
-    hand_back(1);
-    return;
-  }
+  FRA_WSTAMP_WAIT(10)
+  if (fr.n != kMaxBlock) return;  // partial last frames: k_analyze, over the plan's list of them
   constexpr int n = kMaxBlock;
   const int bps = st.bps;
   const LevelCfg cfg = level_cfg(a.level);
@@ -490,17 +502,18 @@ k_analyze_w(JobArgs a, int src) {
   // ---- 1. load + normalise (table gather), OR / min / max
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-  auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx) {
+  auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx, bool first) {
     const int32_t* lut = a.lut + (int64_t)fr.stream * a.lut_stride;
     switch (src) {  // wave-uniform
-      case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
-      case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
-      case ST_U16: wload_lut<ST_U16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
-      default: wload_lut<ST_I16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx); break;
+      case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      case ST_U16: wload_lut<ST_U16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      default: wload_lut<ST_I16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
     }
   };
-  load_samples(orv, vmin, vmax);
+  load_samples(orv, vmin, vmax, true);
   orv = wave_or32(orv);
+  wsync();  // every lane's sample stores before any lane's reads
   FRA_WSTAMP(1)
   vmin = (int32_t)(wave_min32((uint32_t)vmin ^ 0x80000000u) ^ 0x80000000u);
   vmax = (int32_t)(~wave_min32(~((uint32_t)vmax ^ 0x80000000u)) ^ 0x80000000u);
@@ -852,17 +865,19 @@ k_analyze_w(JobArgs a, int src) {
   //  * otherwise (a FIXED order, another window, residuals past 16 bits): the samples (loaded again if the keep
   //    pass overwrote them) and the winner's predictor, the codes ORed straight into the slot in global memory.
   // A kept subframe that is not smaller than VERBATIM, or whose encode would overrun its residuals in the
-  // aliased buffer, goes to k_analyze (redo list)
+  // aliased buffer, takes the second instance after the samples are loaded again: every full frame ends here
   const int type = wtype, o = wo, sh = wsh, ps = wps;
   const bool kept_w = type == 3 && wm == 5 + keep_wi && kept_fit;
-  if (!kept_w && keep_wi >= 0) {  // the keep pass replaced the samples: load them once more
+  auto reload = [&]() {  // the keep pass replaced the samples: load them once more
     wsync();
     uint32_t ov = 0;
     int32_t mn = 0, mx = 0;
-    load_samples(ov, mn, mx);
+    load_samples(ov, mn, mx, false);
+    wsync();
     if (w) shift_wasted();
     wsync();
-  }
+  };
+  if (!kept_w && keep_wi >= 0) reload();
   const int pz = n >> ps;
   const int tl = 8 - ps;                  // log2 chunks per partition (2..8)
   const int ls = tl < 6 ? tl : 6;         // lanes per partition group inside one iteration
@@ -1006,10 +1021,9 @@ k_analyze_w(JobArgs a, int src) {
     const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
     const bool verbatim = exact >= verb;
     const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
-    if (kept && verbatim) {
-      hand_back(6);
-      asm volatile("" ::"v"(pf));
-      return;
+    if (kept && verbatim) {  // VERBATIM wants the samples: the sample path after a reload
+      FRA_WSTAMP_VAL(9, 6)
+      return false;
     }
     if (!kept && verbatim) {  // straight from the samples to the slot
       if (lane == 0) {
@@ -1030,8 +1044,7 @@ k_analyze_w(JobArgs a, int src) {
         }
         slot[jw] = word;
       }
-      asm volatile("" ::"v"(pf));
-      return;
+      return true;
     }
     // code bits of each chunk from the exact pass's sums; the bit position of every iteration's first code
     const uint32_t fbits = (uint32_t)exact;
@@ -1054,14 +1067,13 @@ k_analyze_w(JobArgs a, int src) {
       // the LDS bit buffer aliases the residuals and is filled iteration by iteration, each iteration's
       // residuals read before its words are zeroed and written: iteration j's last word + the spare one must
       // stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a compressible
-      // rest -- the subframe goes to k_analyze)
+      // rest -- the sample path encodes it into the slot instead)
       bool ok = nw + 1 <= kBufWords;  // the whole subframe + the spare word fit the buffer
 #pragma unroll
       for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
       if (!ok) {
-        hand_back(7);
-        asm volatile("" ::"v"(pf));
-        return;
+        FRA_WSTAMP_VAL(9, 7)
+        return false;
       }
     }
     if (lane < kMaxLpc) {
@@ -1143,10 +1155,14 @@ k_analyze_w(JobArgs a, int src) {
         put_codes(slot, j, un);
       }
     }
-    asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
+    return true;
   };
-  if (kept_w) tail(std::true_type{});
-  else tail(std::false_type{});
+  // the kept instance hands a VERBATIM or overrunning subframe to the sample path (samples loaded again)
+  if (!kept_w || !tail(std::true_type{})) {
+    if (kept_w) reload();
+    tail(std::false_type{});
+  }
+  asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
 }
 
 #ifdef FRA_STAMPS

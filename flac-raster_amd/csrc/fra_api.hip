@@ -31,8 +31,8 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
                          hipStream_t s, int max_blocks);
 hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
-hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, int32_t* redo,
-                          unsigned* redo_count, int max_redo_blocks);
+hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, const int32_t* part,
+                          int npart, int max_part_blocks, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join);
 int frame_scan_blocks(int nframes);
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
                              unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
@@ -95,11 +95,13 @@ struct fra_plan {
   float* d_win = nullptr;
   int32_t* d_wrange = nullptr;
   int32_t* d_wplat = nullptr;
-  // redo lists of k_analyze_w (subframes left to k_analyze): per buffer set, entries [frames x cmax] (a
-  // frame group / host band uses the entries of its own frames) and one counter per group slot
-  int32_t* d_redo[2] = {};
-  unsigned* d_redo_cnt[2] = {};
-  int redo_slots = 1;
+  // wave-path plans: the partial subframes k_analyze takes beside k_analyze_w (frame * 8 + channel, ascending;
+  // a launch over frames [f0, f1) passes the entries in [8 f0, 8 f1))
+  std::vector<int32_t> h_part;
+  int32_t* d_part = nullptr;
+  bool wave_ok = false;
+  hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
+  hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -164,14 +166,6 @@ struct fra_plan {
   hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
   bool ana_pending[2] = {false, false};
   bool raster_dirty = false;  // a host raster copy on the plan's stream the norm stream must wait for
-  // Infinity-Cache chunking of a pipelined execute (FRA_CHUNK_MB): the single group split into chunks of
-  // about that many raster bytes; chunk i's norm stage waits for chunk i-2's analysis (cev ring, counted
-  // across executes by chunk_seq), so it runs under chunk i-1's analysis and leaves chunk i's rows in the
-  // 256 MB Infinity Cache for chunk i's analysis; each chunk's frame scan + assembly follow on the pack
-  // stream while its slots are still cache-resident
-  std::vector<Group> chunks;
-  hipEvent_t cev[4] = {};
-  uint64_t chunk_seq = 0;
   bool resync = false;        // serial work was queued on the plan's stream since the last pipelined execute
   // timing
   bool timing = false;
@@ -324,10 +318,10 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_win);
   (void)hipFree(p->d_wrange);
   (void)hipFree(p->d_wplat);
-  for (int b = 0; b < 2; b++) {
-    (void)hipFree(p->d_redo[b]);
-    (void)hipFree(p->d_redo_cnt[b]);
-  }
+  (void)hipFree(p->d_part);
+  if (p->pside) (void)hipStreamDestroy(p->pside);
+  if (p->ev_pfork) (void)hipEventDestroy(p->ev_pfork);
+  if (p->ev_pjoin) (void)hipEventDestroy(p->ev_pjoin);
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
     for (int b = 0; b < 2; b++) {
       (void)hipFree(p->sf2[b]);
@@ -350,9 +344,6 @@ void fra_plan_destroy(fra_plan* p) {
     if (p->ev_pack[b]) (void)hipEventDestroy(p->ev_pack[b]);
     if (p->ev_norm[b]) (void)hipEventDestroy(p->ev_norm[b]);
     if (p->ev_ana[b]) (void)hipEventDestroy(p->ev_ana[b]);
-  }
-  for (auto e : p->cev) {
-    if (e) (void)hipEventDestroy(e);
   }
   if (p->ev_raster) (void)hipEventDestroy(p->ev_raster);
   (void)hipFree(p->d_sf);
@@ -643,11 +634,27 @@ static int plan_build(fra_plan* p) {
       HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
       p->aux.push_back(st);
     }
-    p->redo_slots = (int)std::max(p->groups.size(), p->hbands.size()) + 1;
     if (!p->b32 && j.blocksize == kMaxBlock && j.level >= 3 && j.level <= 6 && j.norm != 0 &&
         elem_size(j.dtype) <= 2 && j.dtype != FRA_F64) {  // plans k_analyze_w may take (wave_path)
-      HIPCHK(hipMalloc(&p->d_redo[0], sizeof(int32_t) * (size_t)std::max(1, nfr) * p->cmax));
-      HIPCHK(hipMalloc(&p->d_redo_cnt[0], sizeof(unsigned) * p->redo_slots));
+      // the partial subframes (frame * 8 + channel, ascending): k_analyze's share of a wave-path launch
+      p->h_part.clear();
+      for (int g = 0; g < nfr; g++) {
+        const FrameDev& fr = p->frames[g];
+        if (fr.n == j.blocksize) continue;
+        const StreamDev& st = p->streams[fr.stream];
+        for (int c = 0; c < (st.ms ? 2 : st.channels); c++) p->h_part.push_back(g * 8 + c);
+      }
+      HIPCHK(hipMalloc(&p->d_part, sizeof(int32_t) * std::max<size_t>(1, p->h_part.size())));
+      if (!p->h_part.empty())
+        HIPCHK(hipMemcpy(p->d_part, p->h_part.data(), sizeof(int32_t) * p->h_part.size(), hipMemcpyHostToDevice));
+      p->wave_ok = true;
+      if (!p->h_part.empty()) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&p->pside, hipStreamNonBlocking, hi));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_pfork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_pjoin, hipEventDisableTiming));
+      }
     }
     p->gev.assign(1 + 2 * p->groups.size(), nullptr);
     for (auto& e : p->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -724,10 +731,6 @@ static int plan_build(fra_plan* p) {
       HIPCHK(hipMalloc(&p->fmeta2[1], sizeof(uint32_t) * kMetaWords * nfr));
       HIPCHK(hipMalloc(&p->fbytes2[1], sizeof(unsigned long long) * (nfr + 1)));
       HIPCHK(hipMalloc(&p->foff2[1], sizeof(unsigned long long) * (nfr + 1)));
-      if (p->d_redo[0]) {
-        HIPCHK(hipMalloc(&p->d_redo[1], sizeof(int32_t) * (size_t)std::max(1, nfr) * p->cmax));
-        HIPCHK(hipMalloc(&p->d_redo_cnt[1], sizeof(unsigned) * p->redo_slots));
-      }
       {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -736,34 +739,6 @@ static int plan_build(fra_plan* p) {
         // start takes the slots the background assembly was using) (r03 v14)
         if (!p->b32)
           for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
-      }
-      {  // Infinity-Cache chunks (windows in order, about FRA_CHUNK_MB of raster each)
-        const char* cm = getenv("FRA_CHUNK_MB");
-        const double mb = cm ? atof(cm) : 0.0;
-        const double fbytes = (double)j.blocksize * std::max(1, j.channels) * elem_size(j.dtype);
-        const int64_t per = mb > 0 ? std::max<int64_t>(1, (int64_t)(mb * 1048576.0 / fbytes)) : (int64_t)nfr;
-        const int nc = (int)std::min<int64_t>(64, (nfr + per - 1) / per);
-        if (nc > 1) {
-          int w = 0, f = 0;
-          for (int c = 0; c < nc && w < (int)p->streams.size(); c++) {
-            const int64_t target = (int64_t)nfr * (c + 1) / nc;
-            fra_plan::Group gr{w, w, f, f};
-            while (w < (int)p->streams.size() && (c == nc - 1 || f < target || gr.f1 == gr.f0)) {
-              f += p->streams[w].nframes;
-              w++;
-              gr.w1 = w;
-              gr.f1 = f;
-            }
-            p->chunks.push_back(gr);
-          }
-          p->chunks.back().w1 = (int)p->streams.size();
-          p->chunks.back().f1 = nfr;
-          // byte offsets of every chunk's first frame (gbase[c]; the chunks scan in order on the pack stream)
-          (void)hipFree(p->d_gbase);
-          HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) *
-                                            (std::max({p->groups.size(), p->hbands.size(), p->chunks.size()}) + 1)));
-          for (auto& e : p->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
       }
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
@@ -899,7 +874,7 @@ static void collect_times(fra_plan* p) {
 // not finish); FRA_ANALYZE_WG=1 keeps every frame on the workgroup kernel (tests compare both)
 static bool wave_path(const fra_plan* p) {
   const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
-  return !wg && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&
+  return !wg && p->wave_ok && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&
          p->job.level >= 3 && p->job.level <= 6;
 }
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
@@ -937,13 +912,13 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
   {
-    // k_analyze_w for the full frames, k_analyze for the subframes it hands back (this group's own redo
-    // entries and counter in the current buffer set)
-    const int b = p->cur;
-    const bool wave = wave_path(p) && p->d_redo[b];
+    // k_analyze_w for the full frames, k_analyze for this group's partial subframes
+    const bool wave = wave_path(p);
+    const auto lo = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f0 * 8);
+    const auto hi = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f1 * 8);
     HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, wave,
-                          wave ? p->d_redo[b] + (size_t)gr.f0 * p->cmax : nullptr,
-                          wave ? p->d_redo_cnt[b] + std::min(gi, p->redo_slots - 1) : nullptr, 8 * p->ncu));
+                          wave ? p->d_part + (lo - p->h_part.begin()) : nullptr, wave ? (int)(hi - lo) : 0,
+                          8 * p->ncu, p->pside, p->ev_pfork, p->ev_pjoin));
   }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
@@ -1015,21 +990,9 @@ int fra_plan_execute(fra_plan* p) {
       HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_raster, 0));
       p->raster_dirty = false;
     }
-    if (p->chunks.empty()) {
-      rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
-                     p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
-      if (rc) return rc;
-    } else {
-      const int nc = (int)p->chunks.size();
-      for (int c = 0; c < nc; c++, p->chunk_seq++) {
-        // chunk i's norm stage after chunk i-2's analysis: one chunk ahead of the analysis, not more
-        if (p->chunk_seq >= 2) HIPCHK(hipStreamWaitEvent(p->nstream, p->cev[(p->chunk_seq - 2) & 3], 0));
-        rc = run_group(p, p->chunks[c], c, nc, as, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, p->pack,
-                       p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(p->cev[p->chunk_seq & 3], as));  // (nothing after the analysis on `as`)
-      }
-    }
+    rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
+                   p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
+    if (rc) return rc;
     p->ana_pending[b] = true;
     HIPCHK(hipEventRecord(p->ev_pack[b], p->pack));
     p->pack_pending[b] = true;

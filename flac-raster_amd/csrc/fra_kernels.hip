@@ -220,16 +220,16 @@ __device__ uint64_t frame_bytes_one(const JobArgs& a, int g) {
 }
 
 // Frame sizes -> byte offsets of a frame group in ONE launch (replaces k_frame_bytes + a library exclusive
-// scan + k_group_offsets: two to three fewer dependent launches per execute): every workgroup sizes 1,024
-// frames (4 per thread), then a single-pass scan with decoupled look-back (Merrill & Garland) over
+// scan + k_group_offsets: two to three fewer dependent launches per execute): every workgroup sizes 256
+// frames (one per thread), then a single-pass scan with decoupled look-back (Merrill & Garland) over
 // workgroups in TICKET order -- a workgroup only ever waits on workgroups that took an earlier ticket, so
-// are already running: no assumption on dispatch order or co-residency.  Look-back words: [63:42] launch tag,
-// [41:40] flag (1 aggregate, 2 inclusive prefix), [39:0] bytes (< 1 TiB per group); the tag makes clearing them unnecessary.
-// add_base: the group's base offset gbase[grp] is ordered before this launch -> final offsets, gbase[grp+1]
-// (+ frame_off[nframes] for the last group, + the host mirror); else group-relative offsets (k_group_offsets
-// adds the base once the previous group is done).
-constexpr int kScanItems = 4;
-constexpr int kScanBlock = 256 * kScanItems;
+// are already running: no assumption on dispatch order or co-residency.  The look-back reads 64
+// predecessors per round (one per lane) and stops at the nearest inclusive prefix.  Look-back words:
+// [63:42] launch tag, [41:40] flag (1 aggregate, 2 inclusive prefix), [39:0] bytes (< 1 TiB per group);
+// the tag makes clearing them unnecessary.  add_base: the group's base offset gbase[grp] is ordered before
+// this launch -> final offsets, gbase[grp+1] (+ frame_off[nframes] for the last group, + the host mirror);
+// else group-relative offsets (k_group_offsets adds the base once the previous group is done).
+constexpr int kScanBlock = 256;
 constexpr uint64_t kScanValMask = (1ull << 40) - 1;
 __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long long* gbase, int grp, int last,
                                                     int add_base, unsigned long long* host_mirror,
@@ -243,16 +243,10 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
   __syncthreads();
   const int t = (int)s_t;  // this workgroup's position in the scan
   const int n = a.frame_count;
-  uint64_t fb[kScanItems];
-  uint64_t loc = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; k++) {
-    const int i = t * kScanBlock + tid * kScanItems + k;
-    fb[k] = i < n ? frame_bytes_one(a, a.frame_base + i) : 0ull;
-    loc += fb[k];
-  }
-  // workgroup-inclusive scan of the per-thread sums: wave scan by DPP-free shuffles, then the 4 wave totals
-  uint64_t incl = loc;
+  const int i = t * kScanBlock + tid;
+  const uint64_t fb = i < n ? frame_bytes_one(a, a.frame_base + i) : 0ull;
+  // workgroup-inclusive scan: wave scan by shuffles, then the 4 wave totals
+  uint64_t incl = fb;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint64_t v = __shfl_up(incl, d, 64);
@@ -266,42 +260,50 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
     wbase += k < wv ? s_w[k] : 0ull;
     agg += s_w[k];
   }
-  if (tid == 0) {
+  if (wv == 0) {
     const uint64_t tg = (uint64_t)(tag & 0x3FFFFFu) << 42;
-    uint64_t excl = 0;
-    if (t == 0) {
-      __hip_atomic_store(&look[0], tg | (2ull << 40) | (agg & kScanValMask), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&look[t], tg | (1ull << 40) | (agg & kScanValMask), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      for (int j = t - 1; j >= 0;) {
-        const uint64_t w = __hip_atomic_load(&look[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t fl = (uint32_t)(w >> 40) & 3u;
-        if ((w & ~((1ull << 42) - 1)) != tg || fl == 0) {
-          __builtin_amdgcn_s_sleep(1);  // workgroup j (an earlier ticket, so running) has not published yet
-          continue;
-        }
-        excl += w & kScanValMask;
-        if (fl == 2) break;
-        j--;
-      }
-      __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELEASE,
+    if (lane == 0)
+      __hip_atomic_store(&look[t], tg | ((t == 0 ? 2ull : 1ull) << 40) | (agg & kScanValMask), __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    for (int j0 = t - 1; j0 >= 0;) {
+      // lane l looks at workgroup j0 - l; before workgroup 0: an inclusive prefix of 0
+      const int j = j0 - lane;
+      const uint64_t w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                : (tg | (2ull << 40));
+      const uint32_t fl = (w & ~((1ull << 42) - 1)) == tg ? (uint32_t)(w >> 40) & 3u : 0u;
+      const uint64_t incm = __ballot(fl == 2), nrdy = __ballot(fl == 0);
+      const int stop = incm ? (int)__builtin_ctzll(incm) : 64;  // the nearest inclusive prefix
+      const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+      if (nrdy & need) {  // a workgroup in the window (an earlier ticket, so running) has not published yet
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint64_t v = lane <= stop ? (w & kScanValMask) : 0ull;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+      excl += v;
+      if (stop < 64) break;
+      j0 -= 64;
     }
-    s_excl = excl;
+    if (lane == 0) {
+      if (t > 0)
+        __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = excl;
+    }
   }
   __syncthreads();
   const uint64_t base = add_base && grp > 0 ? gbase[grp] : 0ull;
-  uint64_t off = base + s_excl + wbase + incl - loc;
-#pragma unroll
-  for (int k = 0; k < kScanItems; k++) {
-    const int i = t * kScanBlock + tid * kScanItems + k;
-    if (i < n) a.frame_off[a.frame_base + i] = off;
-    off += fb[k];
+  const uint64_t off = base + s_excl + wbase + incl - fb;
+  if (i < n) {
+    a.frame_off[a.frame_base + i] = off;
     if (add_base && i == n - 1) {  // the group's end
-      gbase[grp + 1] = off;
-      if (last) a.frame_off[a.nframes_total] = off;
+      const uint64_t end = off + fb;
+      gbase[grp + 1] = end;
+      if (last) a.frame_off[a.nframes_total] = end;
       if (host_mirror) {  // page-locked host copy for the host pipeline (no copy-engine command needed)
-        host_mirror[grp + 1] = off;
+        host_mirror[grp + 1] = end;
         __threadfence_system();
       }
     }

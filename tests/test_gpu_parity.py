@@ -284,6 +284,17 @@ def _noise_then_smooth(n_frames=3, seed=5):
     return x.reshape(1, -1, 4096)
 
 
+@pytest.mark.parametrize("level", [3, 5])
+def test_wave_kernel_noise_verbatim(level):
+    """Full-range noise: k_analyze_w's kept LPC winner is not smaller than VERBATIM, so the wave reloads the
+    samples and writes VERBATIM from them (no hand-back); mixed with smooth bands in the same frames."""
+    rng = np.random.default_rng(11 + level)
+    r = synth_window(4, 5, 3, 256, 512)
+    r[1] = rng.integers(0, 65536, size=r[1].shape, dtype=np.uint16)
+    r[2, :64] = rng.integers(0, 65536, size=(64, 512), dtype=np.uint16)
+    check_windows(r, [(0, 0, 256, 512), (0, 0, 100, 300)], level, 16)
+
+
 @pytest.mark.parametrize("level", [0, 5, 6])
 def test_wave_kernel_incompressible_start(level):
     r = _noise_then_smooth()

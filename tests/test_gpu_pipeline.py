@@ -191,24 +191,19 @@ def test_cross_execute_pipelining_buffers():
         ctx.free(dev)
 
 
-@pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm,chunk_mb", [
-    (4, 4, 4500, 4500, 1024, np.uint16, 5, 16, 0),    # 4 channels, ragged edge tiles (k_analyze<16-bit, lag 8>)
-    (4, 4, 4500, 4500, 1024, np.uint16, 5, 16, 16),   # the same in Infinity-Cache chunks of ~16 MB (10)
-    (4, 2, 4500, 4096, 1000, np.uint16, 5, 16, 0),    # 2 channels: mid-side slot map, odd tile width
-    (4, 2, 4500, 4096, 1000, np.uint16, 5, 16, 5),    # ... chunked
-    (3, 1, 4096, 4096, 512, np.int16, 8, 16, 0),      # lag-12 16-bit instance
-    (5, 2, 4096, 4096, 512, np.float32, 8, 24, 0),    # 32-bps
-    (5, 2, 4096, 4096, 512, np.float32, 8, 24, 20),   # 32-bps, chunked
+@pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm", [
+    (4, 4, 4500, 4500, 1024, np.uint16, 5, 16),    # 4 channels, ragged edge tiles (k_analyze<16-bit, lag 8>)
+    (4, 2, 4500, 4096, 1000, np.uint16, 5, 16),    # 2 channels: mid-side slot map, odd tile width
+    (3, 1, 4096, 4096, 512, np.int16, 8, 16),      # lag-12 16-bit instance
+    (5, 2, 4096, 4096, 512, np.float32, 8, 24),    # 32-bps
 ])
-def test_pipelined_assembly_equals_serial(monkeypatch, kind, bands, H, W, tile, dtype, level, norm, chunk_mb):
+def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level, norm):
     """Pipelined executes run the frame-size chain and the assembly of execute k on the pack stream beside
     execute k+1's analysis (k_assemble_bg on 32-bps plans, k_assemble on 16-bit ones).  The output of
     execute 2, written into an output buffer poisoned after execute 1 and read after a device-wide barrier,
     must be byte-identical to the serial (timing-mode) execute's; so must the plan's own download; and
-    sampled tiles must equal the oracle's frames.  chunk_mb > 0: the pipelined execute runs in
-    Infinity-Cache chunks (FRA_CHUNK_MB, read at plan creation), several frame scans chained on gbase."""
+    sampled tiles must equal the oracle's frames."""
     import ctypes
-    monkeypatch.setenv("FRA_CHUNK_MB", str(chunk_mb))
     hip = ctypes.CDLL("libamdhip64.so")  # the HIP runtime the product library runs on (one per process)
 
     def device_barrier():  # hipDeviceSynchronize: every stream of the device, independent of the plan's sync
