@@ -358,6 +358,25 @@ __device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
 #ifndef FRA_WSTAMP_WAIT
 #define FRA_WSTAMP_WAIT(k) {}
 #endif
+// phase-stop diagnostic builds (csrc/Makefile `wstops`, tools/pmc_stall_phases.sh): every subframe is first
+// described as VERBATIM (valid sizes: the frame scan and the assembly stay inside their buffers; the bytes
+// are meaningless), then the wave returns after phase k, keeping that phase's results alive through the
+// descriptor's unused cval
+#ifdef FRA_WSTOP
+#define FRA_WSTOP_AT(k, keep)                      \
+  if (FRA_WSTOP == (k)) {                          \
+    if (lane == 0) d->cval = (int32_t)(keep);      \
+    return;                                        \
+  }
+#define FRA_WSTOP_AT_T(k, keep)                    \
+  if (FRA_WSTOP == (k)) {                          \
+    if (lane == 0) d->cval = (int32_t)(keep);      \
+    return true;                                   \
+  }
+#else
+#define FRA_WSTOP_AT(k, keep)
+#define FRA_WSTOP_AT_T(k, keep)
+#endif
 
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
 // lane l loads the 8-byte vectors l + 64k (all issued before the first use), gathers each sample's audio
@@ -466,10 +485,8 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
 }  // namespace
 
 
-// prefetch distance in waves: ~a quarter of the 4,096 waves resident chip-wide (16 per CU), so the rows are
-// in L2 (1 MiB of rows per XCD in flight) when that wave starts
-constexpr int kWPrefetch = 1024;
-
+// (no L2 prefetch of a later wave's rows, unlike k_analyze: measured slower here at every distance,
+// profiles/r04_ab_wave_prefetch_distance.txt)
 template <int MAXLAG>
 // occupancy target: 8 KiB of LDS lets 20 waves share a CU; <= 96 VGPRs make it 5 per SIMD
 #ifndef FRA_W_WAVES
@@ -494,11 +511,13 @@ k_analyze_w(JobArgs a, int src) {
   const LevelCfg cfg = level_cfg(a.level);
   SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
   uint32_t* const slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
+#ifdef FRA_WSTOP
+  if (lane == 0) {
+    d->type = 1; d->order = 0; d->wasted = 0; d->sbps = (uint8_t)bps; d->cval = 0; d->porder = 0;
+    d->method = 0; d->precision = 0; d->shift = 0; d->bits = 8u + (uint32_t)n * (uint32_t)bps;
+  }
+#endif
 
-  // L2 prefetch of the rows of the subframe kWPrefetch waves ahead, issued first: its metadata loads overlap
-  // this wave's own, and its row loads land with this wave's (in-order vmcnt)
-  const uint32_t pf = (src == ST_U16 || src == ST_I16) ? prefetch_rows<uint16_t, kWPrefetch>(a, lane)
-                                                       : prefetch_rows<uint8_t, kWPrefetch>(a, lane);
   // ---- 1. load + normalise (table gather), OR / min / max
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
@@ -517,6 +536,7 @@ k_analyze_w(JobArgs a, int src) {
   FRA_WSTAMP(1)
   vmin = (int32_t)(wave_min32((uint32_t)vmin ^ 0x80000000u) ^ 0x80000000u);
   vmax = (int32_t)(~wave_min32(~((uint32_t)vmax ^ 0x80000000u)) ^ 0x80000000u);
+  FRA_WSTOP_AT(1, orv ^ (uint32_t)vmin ^ (uint32_t)vmax ^ sw[lane] ^ sw[2047 - lane])
 
   // ---- 2. CONSTANT / wasted bits (3.2, 3.3)
   if (vmin == vmax) {
@@ -528,7 +548,6 @@ k_analyze_w(JobArgs a, int src) {
       slot[0] = (uint32_t)(blob >> 32);
       slot[1] = (uint32_t)blob;
     }
-    asm volatile("" ::"v"(pf));
     return;
   }
   const int w = __builtin_ctz(orv);
@@ -581,6 +600,7 @@ k_analyze_w(JobArgs a, int src) {
     }
   }
   FRA_WSTAMP(2)
+  FRA_WSTOP_AT(2, pfix[0] ^ pfix[1] ^ pfix[2] ^ pfix[3] ^ pfix[4])
 
   // ---- running winner (FRA-1 3.8: first minimal estimate in model order)
   uint32_t west = 0xFFFFFFFFu;
@@ -619,6 +639,7 @@ k_analyze_w(JobArgs a, int src) {
   }
 #endif
   FRA_WSTAMP(3)
+  FRA_WSTOP_AT(3, pf1 ^ pf2 ^ (uint32_t)(g1 * 8 + g2))
   // ---- 3. LPC analysis per apodization window (3.4-3.7): lane 16 wi + o_l of window wi's lane group holds
   // that window's model (order o_l, quantised q, shift qsh, ok)
   int nlpc = 0;
@@ -727,6 +748,14 @@ k_analyze_w(JobArgs a, int src) {
         }
       }
       FRA_WSTAMP(4)
+#ifdef FRA_WSTOP
+      {
+        uint64_t kx = 0;
+#pragma unroll
+        for (int l = 0; l < NL; l++) kx ^= (uint64_t)__double_as_longlong(acl[l]);
+        FRA_WSTOP_AT(4, kx ^ (kx >> 32))
+      }
+#endif
       // Levinson-Durbin, order choice and quantisation of up to 4 windows at once: window wi on lanes
       // 16 wi .. +15 (the same op sequence per lane); lane 16 wi + o holds order o's row and quantisation
       const int gw = lane >> 4, lo = lane & 15;
@@ -767,6 +796,18 @@ k_analyze_w(JobArgs a, int src) {
     }
   }
   FRA_WSTAMP(5)
+#ifdef FRA_WSTOP
+  {
+    uint32_t kx = 0;
+#pragma unroll
+    for (int wi = 0; wi < kWinW; wi++) {
+      kx ^= (uint32_t)msh[wi] ^ ((uint32_t)mo[wi] << 8) ^ (mok[wi] ? 1u << 16 : 0u);
+#pragma unroll
+      for (int jx = 0; jx < 8; jx++) kx ^= (uint32_t)mq[wi][jx] << jx;
+    }
+    FRA_WSTOP_AT(5, kx)
+  }
+#endif
 
   // ---- 4+5. the candidates in model order -- FIXED g1, g2, then each window's LPC model -- one partition
   // search each (one code body); an LPC model first gets its residual sums at the finest partitions.
@@ -858,6 +899,7 @@ k_analyze_w(JobArgs a, int src) {
   }
 
   FRA_WSTAMP(6)
+  FRA_WSTOP_AT(6, west ^ (uint32_t)wm ^ (uint32_t)wps)
   // ---- 6. the winner's zig-zag residuals, exact Rice bits with each partition's parameter refined (3.9),
   // encode (RFC 9639 9.2).  Two instances:
   //  * kept (the common case): the winner is the LPC model of the keep pass and every residual fits 16 bits:
@@ -1019,6 +1061,7 @@ k_analyze_w(JobArgs a, int src) {
     const bool big = __any(bigl);
     const uint64_t rtot = (uint64_t)wave_sum32(bitsl) + (uint64_t)npp * (big ? 5 : 4) + 6;
     const uint64_t exact = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + rtot;
+    FRA_WSTOP_AT_T(7, exact)
     const bool verbatim = exact >= verb;
     const uint32_t smask = (1u << sbps) - 1u;  // sbps <= 16
     if (kept && verbatim) {  // VERBATIM wants the samples: the sample path after a reload
@@ -1162,7 +1205,6 @@ k_analyze_w(JobArgs a, int src) {
     if (kept_w) reload();
     tail(std::false_type{});
   }
-  asm volatile("" ::"v"(pf));  // (the prefetch words: kept alive, long landed)
 }
 
 #ifdef FRA_STAMPS

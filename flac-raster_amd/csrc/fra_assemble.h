@@ -149,6 +149,13 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM
   // slot of output channels 0 / 1 (k_frame_scan: identity unless a mid-side assignment was chosen)
   const uint32_t smap = C == 2 ? (uint32_t)__builtin_amdgcn_readfirstlane(gmeta[kHdrWords - 1]) : 0u;
   auto vslot = [&](int oc) -> int { return C == 2 ? (int)((smap >> (8 * oc)) & 0xFFu) : oc; };
+  {  // a frame whose sizes would leave the output or its slots (only a corrupt descriptor can) is not written
+    bool inb = F + L + 2 <= a.out_cap && C >= 1 && C <= kMaxChannels;
+#pragma unroll
+    for (int i = 0; i < kMaxChannels; i++)
+      inb = inb && (i >= C || sg[i + 2] - sg[i + 1] <= 32u * (uint32_t)a.tmp_stride);
+    if (!inb) return;
+  }
 #ifdef FRA_GUARD
   const uint64_t TOT = a.out_cap;  // frame_off[nframes_total] is final only after the last frame group
   const uint64_t SLOTW = (uint64_t)a.nframes_total * a.cmax * a.tmp_stride;

@@ -3,6 +3,7 @@
 # PMC pass per library with 8 SQ counters (WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY,
 # quad-cycles; MI355X_MICROARCH.md "rocprofv3 PMC slots").  Post-process: tools/pmc_stall_table.py.
 #   bash tools/pmc_stall_phases.sh <out-subdir> [config] [stops...]      (GPU box, repo root)
+#   STOPLIB=wstop: the k_analyze_w phase-stop builds (csrc/Makefile `wstops`) instead of k_analyze's `diag`
 set -o pipefail
 TAG=$1
 CFG=${2:-c4}
@@ -13,7 +14,7 @@ mkdir -p $OUT
 cd /tmp
 export TMPDIR=/tmp
 for k in $STOPS; do
-  if [ $k = full ]; then LIB=-; else LIB=$GRAFT_REPO_ROOT/flac-raster_amd/flac_raster/_lib/diag/libflac_raster_amd_diag$k.so; fi
+  if [ $k = full ]; then LIB=-; else LIB=$GRAFT_REPO_ROOT/flac-raster_amd/flac_raster/_lib/diag/libflac_raster_amd_${STOPLIB:-diag}$k.so; fi
   timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
     --output-format csv -d $OUT/a$k -o run -- python $GRAFT_REPO_ROOT/tools/diag_phases.py $LIB $CFG > $OUT/a$k.log 2>&1 \

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Stall table from tools/pmc_stall_phases.sh output: per phase stop, k_analyze counters per wave (median
 launch) and the WAVE_CYCLES split WAIT_ANY (parked: s_waitcnt / barrier) + WAIT_INST_ANY (issue stall) +
-ACTIVE_INST_ANY (issuing), plus the per-phase deltas.  Usage: pmc_stall_table.py <dir> [kernel]"""
+ACTIVE_INST_ANY (issuing), plus the per-phase deltas.  Usage: pmc_stall_table.py <dir> [kernel]
+(kernel k_analyze_w: the phase names of its FRA_WSTOP builds)"""
 import csv
 import sys
 from pathlib import Path
@@ -10,6 +11,9 @@ ORDER = ["1", "9", "8", "2", "3", "5", "6", "7", "4", "full"]
 NAMES = {"1": "load+normalise", "9": "FIXED sums", "8": "autocorrelation", "2": "LD/quantise (+FIXED search)",
          "3": "LPC residual sums", "5": "partition search", "6": "winner residuals + Rice sums",
          "7": "exact bits + scan", "4": "(slow path)", "full": "encode + slot write"}
+WORDER = ["1", "2", "3", "4", "5", "6", "7", "full"]
+WNAMES = {"1": "load + LUT + reduce", "2": "FIXED sums", "3": "FIXED guesses", "4": "autocorrelation",
+          "5": "Levinson + quantise", "6": "LPC sums + searches", "7": "winner exact pass", "full": "encode + slot"}
 
 
 def load(d, kernel):
@@ -30,8 +34,12 @@ def load(d, kernel):
 def main():
     d = Path(sys.argv[1])
     kernel = sys.argv[2] if len(sys.argv) > 2 else "k_analyze"
+    global NAMES
+    order = ORDER
+    if kernel == "k_analyze_w":
+        order, NAMES = WORDER, WNAMES
     rows = []
-    for s in ORDER:
+    for s in order:
         a, b = d / f"a{s}", d / f"b{s}"
         if not a.exists():
             continue
