@@ -910,6 +910,7 @@ k_analyze_w(JobArgs a, int src) {
   // aliased buffer, takes the second instance after the samples are loaded again: every full frame ends here
   const int type = wtype, o = wo, sh = wsh, ps = wps;
   const bool kept_w = type == 3 && wm == 5 + keep_wi && kept_fit;
+  FRA_WSTAMP_VAL(9, kept_w ? 0 : (type != 3 ? 3 : (wm != 5 + keep_wi ? 4 : 5)))  // why the sample path
   auto reload = [&]() {  // the keep pass replaced the samples: load them once more
     wsync();
     uint32_t ov = 0;
@@ -935,8 +936,10 @@ k_analyze_w(JobArgs a, int src) {
     }
     fra_short2 Q[4];
     q_pairs_rev<4>(wq, Q);
-    // the residuals of chunk 64 j + lane (warm-up positions 0)
-    auto residuals = [&](int j, uint32_t (&un)[kChunk]) {
+    // the residuals of chunk 64 j + lane (warm-up positions 0).  Sample path: chunk 64 j - 1's last 12 samples
+    // (lane 0's look-back) come from cy, lane 63's words of the previous call, so iteration j - 1's bit-buffer
+    // words may already cover that chunk (calls in order j = 0..3)
+    auto residuals = [&](int j, uint32_t (&un)[kChunk], uint32_t (&cy)[6]) {
       const int t = 64 * j + lane;
       if (kept) {  // 8 dwords of int16 pairs
         const uint32_t* po = sw + 8 * lane + kWIterDw * j;
@@ -952,6 +955,12 @@ k_analyze_w(JobArgs a, int src) {
       }
       uint32_t D[14];
       wread_d14(sw, lane, j, D);
+      if (j > 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) D[k] = lane == 0 ? cy[k] : D[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) cy[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[8 + k], 63);
       if (type == 3) {
 #pragma unroll
         for (int jj = 0; jj < kChunk; jj++) un[jj] = zz32(sample_at(D, 12 + jj) - (pred_raw<4>(D, 12 + jj, Q) >> sh));
@@ -978,11 +987,12 @@ k_analyze_w(JobArgs a, int src) {
     uint32_t bitsl = 0;         // exact bits of the partitions this lane leads
     bool bigl = false;
     uint64_t E[3] = {0, 0, 0};  // partitions spanning iterations (ps <= 1): running sums
+    uint32_t cyx[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < kWIters; j++) {
       const int t = 64 * j + lane;
       uint32_t un[kChunk];
-      residuals(j, un);
+      residuals(j, un, cyx);
       const int pidx = t >> tl;
       const int k0 = __shfl((int)wk, pidx & 63, 64);
       const int km = k0 > 0 ? k0 - 1 : 0;
@@ -1106,18 +1116,17 @@ k_analyze_w(JobArgs a, int src) {
       totl[j] = f + (uint32_t)(kChunk - (t == 0 ? o : 0)) * (kcur + 1u) + (pstart ? (uint32_t)pb : 0u);
       B[j + 1] = B[j] + wave_sum32(totl[j]);
     }
-    if (kept) {
-      // the LDS bit buffer aliases the residuals and is filled iteration by iteration, each iteration's
-      // residuals read before its words are zeroed and written: iteration j's last word + the spare one must
-      // stay below chunk 64 (j + 1)'s first word (else -- a poorly compressible start before a compressible
-      // rest -- the sample path encodes it into the slot instead)
-      bool ok = nw + 1 <= kBufWords;  // the whole subframe + the spare word fit the buffer
+    // the LDS bit buffer aliases the residuals (kept) or samples and is filled iteration by iteration, each
+    // iteration's residuals computed before its words are zeroed and written: iteration j's last word + the
+    // spare one must stay below chunk 64 (j + 1)'s first word.  Else (a poorly compressible start before a
+    // compressible rest) the kept instance hands over to the sample path, which ORs the codes into the slot
+    // in global memory
+    bool inlds = nw + 1 <= kBufWords;  // the whole subframe + the spare word fit the buffer
 #pragma unroll
-      for (int j = 0; j + 1 < kWIters; j++) ok = ok && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
-      if (!ok) {
-        FRA_WSTAMP_VAL(9, 7)
-        return false;
-      }
+    for (int j = 0; j + 1 < kWIters; j++) inlds = inlds && (B[j + 1] - 1) / 32 + 2 <= (uint32_t)sdw(64 * (j + 1), 0);
+    if (kept && !inlds) {
+      FRA_WSTAMP_VAL(9, 7)
+      return false;
     }
     if (lane < kMaxLpc) {
       int32_t cv = 0;
@@ -1169,13 +1178,14 @@ k_analyze_w(JobArgs a, int src) {
         }
       }
     };
-    if (kept) {
+    uint32_t cye[6] = {0, 0, 0, 0, 0, 0};
+    if (kept || inlds) {
       uint32_t* const buf = sw;
       uint32_t Z = 0;  // words [0, Z) are zeroed (and possibly written)
 #pragma unroll
       for (int j = 0; j < kWIters; j++) {
         uint32_t un[kChunk];
-        residuals(j, un);
+        residuals(j, un, cye);
         wsync();  // every lane's reads of this iteration's residuals precede the zeroing
         const uint32_t Zend = j == kWIters - 1 ? nw + 1 : (B[j + 1] - 1) / 32 + 2;
         for (uint32_t jw = Z + lane; jw < Zend; jw += 64) buf[jw] = 0u;
@@ -1187,14 +1197,14 @@ k_analyze_w(JobArgs a, int src) {
       wsync();
       for (uint32_t jw = lane; jw < nw; jw += 64) slot[jw] = buf[jw];
       FRA_WSTAMP(8)
-    } else {  // the samples stay: codes ORed into the zeroed slot (global atomics)
+    } else {  // codes ORed into the zeroed slot (global atomics)
       for (uint32_t jw = lane; jw <= nw; jw += 64) slot[jw] = 0u;  // (nw + 1 <= tmp_stride)
       __threadfence();
       put_header(slot);
 #pragma unroll 1
       for (int j = 0; j < kWIters; j++) {
         uint32_t un[kChunk];
-        residuals(j, un);
+        residuals(j, un, cye);
         put_codes(slot, j, un);
       }
     }

@@ -260,15 +260,19 @@ def test_wave_kernel_levels_dtypes(level, dtype):
     check_windows(r, [(0, 0, 300, 700), (0, 0, 64, 64), (17, 9, 131, 257)], level, 16)
 
 
-def test_wave_kernel_equals_workgroup_kernel(monkeypatch):
-    """k_analyze_w and k_analyze (FRA_ANALYZE_WG=1) produce the same bytes on a C4-like scene."""
+@pytest.mark.parametrize("kind,bands,tile", [(4, 4, 1024), (3, 1, 512)])
+def test_wave_kernel_equals_workgroup_kernel(monkeypatch, kind, bands, tile):
+    """k_analyze_w and k_analyze (FRA_ANALYZE_WG=1) produce the same bytes on a C4-like scene and on a C3-like
+    int16 DEM (whose LPC residuals often pass 2^16: the sample path, codes in the LDS bit buffer)."""
     H = W = 1300
-    r = synth_window(4, 99, 4, H, W)
-    wins = tiles(H, W, 1024)
+    r = synth_window(kind, 99, bands, H, W)
+    wins = tiles(H, W, tile)
     _, wave = N.encode_windows(r, wins, level=5, norm=16)
     monkeypatch.setenv("FRA_ANALYZE_WG", "1")
     _, wg = N.encode_windows(r, wins, level=5, norm=16)
     assert wave == wg
+    if kind == 3:  # and against the oracle on a few tiles
+        check_windows(r, wins[:2] + wins[-1:], 5, 16)
 
 
 def _noise_then_smooth(n_frames=3, seed=5):

@@ -72,7 +72,7 @@ why = st[:, 9][st[:, 0] > 0]
 names = {1: "partial frame", 2: "no LPC model", 3: "FIXED wins", 4: "other LPC window wins", 5: "residual >= 2^16",
          6: "not below VERBATIM", 7: "encode would overrun"}
 hb = {names.get(int(k), str(k)): int((why == k).sum()) for k in np.unique(why) if k}
-print(f"handed back to k_analyze: {int((why > 0).sum())} of {len(why)} stamped waves: {hb}")
+print(f"sample-path (non-kept) subframes: {int((why > 0).sum())} of {len(why)} stamped waves: {hb}")
 s0 = st[full, 0]
 span = st[full, 8].max() - s0.min()
 print(f"stamped span {span} cycles; mean resident (stamped) waves {tot.sum() / span:.1f}")
