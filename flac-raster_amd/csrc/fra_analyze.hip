@@ -523,7 +523,8 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 // next workgroups by dispatch order (not in the redo-list mode)
 template <bool B32, int MAXLAG>
 __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, const int g, const int cy, const int rot,
-                                           const bool pf_allowed, AnalyzeSmem<B32, MAXLAG>& S) {
+                                           const bool pf_allowed) {
+  __shared__ AnalyzeSmem<B32, MAXLAG> S;  // (declared here, not passed by reference: keeps every access in LDS)
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
   // 7-wave 16-bit instance
@@ -704,7 +705,11 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
         // plateau of exact 1.0f (tukey and partial tukeys) the product is the sample itself:
         // no load, and no multiply when the whole wave's span lies inside (bit-identical partials)
         const int32_t* wpl = a.wplat + 2 * ((size_t)fr.win * a.nwin + wi);
+#ifndef FRA_NOPLAT
         const bool plat = i0 >= wpl[0] && i0 + kChunk + MAXLAG <= wpl[1];
+#else
+        const bool plat = false && wpl;
+#endif
         float wcoef[kChunk + MAXLAG];
         if (plat) {
 #pragma unroll
@@ -1476,19 +1481,16 @@ read_x28(S.smp, t, x);
 
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
-  __shared__ AnalyzeSmem<B32, MAXLAG> S;
-  if (a.redo) {
-    // list mode (beside k_analyze_w): the partial subframes, entry = frame * 8 + channel, by a grid of
-    // workgroups striding over the list
-    for (int i = (int)blockIdx.x; i < a.redo_n; i += (int)gridDim.x) {
-      __syncthreads();  // the previous entry's LDS is dead
-      const int e = __builtin_amdgcn_readfirstlane(a.redo[i]);
-      analyze_wg<B32, MAXLAG>(a, src, e >> 3, e & 7, i & 3, false, S);
-    }
-    return;
+  // list mode (beside k_analyze_w): workgroup i takes entry i of the partial-subframe list (frame * 8 +
+  // channel); one call site, so the body is inlined once
+  int g = a.frame_base + (int)blockIdx.x, c = (int)blockIdx.y;
+  if (!B32 && MAXLAG == 8 && a.redo) {  // (only this instance runs beside k_analyze_w)
+    const int e = __builtin_amdgcn_readfirstlane(a.redo[blockIdx.x]);
+    g = e >> 3;
+    c = e & 7;
   }
-  analyze_wg<B32, MAXLAG>(a, src, a.frame_base + (int)blockIdx.x, (int)blockIdx.y, (int)((blockIdx.x + blockIdx.y) & 3),
-                          true, S);
+  analyze_wg<B32, MAXLAG>(a, src, g, c, (int)((blockIdx.x + blockIdx.y) & 3),
+                          B32 || MAXLAG != 8 || a.redo == nullptr);
 }
 
 #ifdef FRA_STAMPS
@@ -1509,6 +1511,19 @@ hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStr
 
 // wave: 16-bit plans whose full frames k_analyze_w takes (fra_api.hip wave_path): k_analyze_w over the launch's
 // frames, k_analyze over `part` (the launch's npart partial subframes, frame * 8 + channel), both complete
+// k_analyze over a list of partial subframes (frame * 8 + channel) on stream s (the pipelined execute runs it
+// on the norm stream right after the norm stage, a whole execute ahead of the frame scan that needs it)
+hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, int npart, int max_part_blocks,
+                               hipStream_t s) {
+  if (npart <= 0) return hipSuccess;
+  JobArgs wa = a;
+  wa.redo = part;
+  wa.redo_n = npart;
+  (void)max_part_blocks;
+  k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, s>>>(wa, src);  // one workgroup per entry
+  return hipGetLastError();
+}
+
 // (side, ev_fork, ev_join: the partial subframes run on the side stream beside k_analyze_w -- a handful of
 // workgroups that would otherwise idle the device for their whole latency after it -- joined back before the
 // caller's next work on s; null side: after k_analyze_w on s)
@@ -1525,7 +1540,7 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
       JobArgs wa = a;
       wa.redo = part;
       wa.redo_n = npart;
-      k_analyze<false, 8><<<(unsigned)std::min(npart, max_part_blocks), kThreads, 0, ps>>>(wa, src);
+      k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
     };
     const bool fork = npart > 0 && side;
     if (fork) {

@@ -33,6 +33,8 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, const int32_t* part,
                           int npart, int max_part_blocks, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join);
+hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, int npart, int max_part_blocks,
+                               hipStream_t s);
 int frame_scan_blocks(int nframes);
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
                              unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
@@ -102,6 +104,7 @@ struct fra_plan {
   bool wave_ok = false;
   hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
   hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+  hipEvent_t ev_part[2] = {};  // pipelined: the partial subframes of buffer set b done (on the norm stream)
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -322,6 +325,8 @@ void fra_plan_destroy(fra_plan* p) {
   if (p->pside) (void)hipStreamDestroy(p->pside);
   if (p->ev_pfork) (void)hipEventDestroy(p->ev_pfork);
   if (p->ev_pjoin) (void)hipEventDestroy(p->ev_pjoin);
+  for (auto e : p->ev_part)
+    if (e) (void)hipEventDestroy(e);
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
     for (int b = 0; b < 2; b++) {
       (void)hipFree(p->sf2[b]);
@@ -621,7 +626,7 @@ static int plan_build(fra_plan* p) {
     build_host_bands(p, nfr);
     // look-back words (zero: no tag yet) and tickets of every scan slot, sized for the whole plan
     const int nslot = (int)p->groups.size();
-    p->look_stride = std::max(1, frame_scan_blocks(nfr));
+    p->look_stride = std::max(64, frame_scan_blocks(nfr));  // (any group of <= nfr frames: <= 64 or nfr's count)
     HIPCHK(hipMalloc(&p->d_look, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
     HIPCHK(hipMemset(p->d_look, 0, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
     HIPCHK(hipMalloc(&p->d_ticket, sizeof(unsigned) * nslot));
@@ -745,6 +750,7 @@ static int plan_build(fra_plan* p) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_pack[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&p->ev_norm[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&p->ev_ana[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&p->ev_part[b], hipEventDisableTiming));
       }
     }
   }
@@ -903,22 +909,31 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     HIPCHK(launch_norm_finalize(ma, nc, nst_s));
     HIPCHK(launch_norm_lut(p->src, ma, nc, nst_s));
   }
-  if (norm_st) {
-    HIPCHK(hipEventRecord(ev_norm, norm_st));
-    HIPCHK(hipStreamWaitEvent(st, ev_norm, 0));
-  }
-  if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
   JobArgs ga = a;
   ga.frame_base = gr.f0;
   ga.frame_count = nf;
+  // wave path: k_analyze_w for the full frames, k_analyze for this group's partial subframes -- pipelined, on
+  // the norm stream right after the norm stage (a whole execute before the frame scan that waits for them),
+  // else beside k_analyze_w on the side stream
+  const bool wave = wave_path(p);
+  const auto plo = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f0 * 8);
+  const auto phi = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f1 * 8);
+  const int npart = wave ? (int)(phi - plo) : 0;
+  const int32_t* part = wave ? p->d_part + (plo - p->h_part.begin()) : nullptr;
+  const hipEvent_t ev_part = (norm_st && npart > 0) ? p->ev_part[p->cur] : nullptr;
+  if (norm_st) {
+    HIPCHK(hipEventRecord(ev_norm, norm_st));
+    HIPCHK(hipStreamWaitEvent(st, ev_norm, 0));
+    if (ev_part) {
+      HIPCHK(launch_analyze_part(p->src, ga, part, npart, 8 * p->ncu, norm_st));
+      HIPCHK(hipEventRecord(ev_part, norm_st));
+    }
+  }
+  if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
   {
-    // k_analyze_w for the full frames, k_analyze for this group's partial subframes
-    const bool wave = wave_path(p);
-    const auto lo = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f0 * 8);
-    const auto hi = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f1 * 8);
     HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, wave,
-                          wave ? p->d_part + (lo - p->h_part.begin()) : nullptr, wave ? (int)(hi - lo) : 0,
-                          8 * p->ncu, p->pside, p->ev_pfork, p->ev_pjoin));
+                          ev_part ? nullptr : part, ev_part ? 0 : npart, 8 * p->ncu, p->pside, p->ev_pfork,
+                          p->ev_pjoin));
   }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
@@ -933,6 +948,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     st = pack_st;
     pack_st = nullptr;
   }
+  if (ev_part) HIPCHK(hipStreamWaitEvent(st, ev_part, 0));  // the partial subframes (norm stream) are done
   // frame sizes and offsets: one k_frame_scan; with the group's base already ordered (first / only group,
   // host bands on one stream) it writes the final offsets itself, else k_group_offsets adds the base once
   // the previous group has published it

@@ -220,17 +220,18 @@ __device__ uint64_t frame_bytes_one(const JobArgs& a, int g) {
 }
 
 // Frame sizes -> byte offsets of a frame group in ONE launch (replaces k_frame_bytes + a library exclusive
-// scan + k_group_offsets: two to three fewer dependent launches per execute): every workgroup sizes 256
-// frames (one per thread), then a single-pass scan with decoupled look-back (Merrill & Garland) over
+// scan + k_group_offsets: two to three fewer dependent launches per execute): every workgroup sizes 256 x ITEMS
+// frames, then a single-pass scan with decoupled look-back (Merrill & Garland) over
 // workgroups in TICKET order -- a workgroup only ever waits on workgroups that took an earlier ticket, so
 // are already running: no assumption on dispatch order or co-residency.  The look-back reads 64
 // predecessors per round (one per lane) and stops at the nearest inclusive prefix.  Look-back words:
 // [63:42] launch tag, [41:40] flag (1 aggregate, 2 inclusive prefix), [39:0] bytes (< 1 TiB per group);
-// the tag makes clearing them unnecessary.  add_base: the group's base offset gbase[grp] is ordered before
+// the tag makes clearing them unnecessary; each word carries its own payload, so relaxed device-scope atomics
+// suffice (no acquire/release cache maintenance per look-back round).  add_base: the group's base offset gbase[grp] is ordered before
 // this launch -> final offsets, gbase[grp+1] (+ frame_off[nframes] for the last group, + the host mirror);
 // else group-relative offsets (k_group_offsets adds the base once the previous group is done).
-constexpr int kScanBlock = 256;
 constexpr uint64_t kScanValMask = (1ull << 40) - 1;
+template <int ITEMS>  // frames per thread (contiguous): 256 * ITEMS per workgroup
 __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long long* gbase, int grp, int last,
                                                     int add_base, unsigned long long* host_mirror,
                                                     unsigned long long* look, unsigned* ticket, unsigned tbase,
@@ -243,10 +244,15 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
   __syncthreads();
   const int t = (int)s_t;  // this workgroup's position in the scan
   const int n = a.frame_count;
-  const int i = t * kScanBlock + tid;
-  const uint64_t fb = i < n ? frame_bytes_one(a, a.frame_base + i) : 0ull;
-  // workgroup-inclusive scan: wave scan by shuffles, then the 4 wave totals
-  uint64_t incl = fb;
+  const int i0 = (t * 256 + tid) * ITEMS;
+  uint64_t fb[ITEMS], loc = 0;
+#pragma unroll
+  for (int k = 0; k < ITEMS; k++) {
+    fb[k] = i0 + k < n ? frame_bytes_one(a, a.frame_base + i0 + k) : 0ull;
+    loc += fb[k];
+  }
+  // workgroup-inclusive scan of the per-thread sums: wave scan by shuffles, then the 4 wave totals
+  uint64_t incl = loc;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint64_t v = __shfl_up(incl, d, 64);
@@ -263,13 +269,13 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
   if (wv == 0) {
     const uint64_t tg = (uint64_t)(tag & 0x3FFFFFu) << 42;
     if (lane == 0)
-      __hip_atomic_store(&look[t], tg | ((t == 0 ? 2ull : 1ull) << 40) | (agg & kScanValMask), __ATOMIC_RELEASE,
+      __hip_atomic_store(&look[t], tg | ((t == 0 ? 2ull : 1ull) << 40) | (agg & kScanValMask), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     for (int j0 = t - 1; j0 >= 0;) {
       // lane l looks at workgroup j0 - l; before workgroup 0: an inclusive prefix of 0
       const int j = j0 - lane;
-      const uint64_t w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+      const uint64_t w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                 : (tg | (2ull << 40));
       const uint32_t fl = (w & ~((1ull << 42) - 1)) == tg ? (uint32_t)(w >> 40) & 3u : 0u;
       const uint64_t incm = __ballot(fl == 2), nrdy = __ballot(fl == 0);
@@ -288,23 +294,27 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
     }
     if (lane == 0) {
       if (t > 0)
-        __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELEASE,
+        __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       s_excl = excl;
     }
   }
   __syncthreads();
   const uint64_t base = add_base && grp > 0 ? gbase[grp] : 0ull;
-  const uint64_t off = base + s_excl + wbase + incl - fb;
-  if (i < n) {
-    a.frame_off[a.frame_base + i] = off;
-    if (add_base && i == n - 1) {  // the group's end
-      const uint64_t end = off + fb;
-      gbase[grp + 1] = end;
-      if (last) a.frame_off[a.nframes_total] = end;
-      if (host_mirror) {  // page-locked host copy for the host pipeline (no copy-engine command needed)
-        host_mirror[grp + 1] = end;
-        __threadfence_system();
+  uint64_t off = base + s_excl + wbase + incl - loc;
+#pragma unroll
+  for (int k = 0; k < ITEMS; k++) {
+    const int i = i0 + k;
+    if (i < n) {
+      a.frame_off[a.frame_base + i] = off;
+      off += fb[k];
+      if (add_base && i == n - 1) {  // the group's end
+        gbase[grp + 1] = off;
+        if (last) a.frame_off[a.nframes_total] = off;
+        if (host_mirror) {  // page-locked host copy for the host pipeline (no copy-engine command needed)
+          host_mirror[grp + 1] = off;
+          __threadfence_system();
+        }
       }
     }
   }
@@ -387,13 +397,22 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
   return hipGetLastError();
 }
 
-int frame_scan_blocks(int nframes) { return (nframes + kScanBlock - 1) / kScanBlock; }
+// frames per thread: <= ~64 workgroups for large groups (fewer look-back rounds and fewer background
+// workgroups beside the next execute's analysis), one per thread for small ones (latency)
+static int scan_items(int nframes) { return nframes <= 256 * 64 ? 1 : (nframes <= 4 * 256 * 64 ? 4 : 16); }
+int frame_scan_blocks(int nframes) {
+  const int per = 256 * scan_items(nframes);
+  return (nframes + per - 1) / per;
+}
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
                              unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
                              unsigned tbase, unsigned tag, hipStream_t s) {
-  if (a.frame_count > 0)
-    k_frame_scan<<<frame_scan_blocks(a.frame_count), 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look,
-                                                                  ticket, tbase, tag);
+  if (a.frame_count > 0) {
+    const int it = scan_items(a.frame_count), nb = frame_scan_blocks(a.frame_count);
+    if (it == 1) k_frame_scan<1><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
+    else if (it == 4) k_frame_scan<4><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
+    else k_frame_scan<16><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
+  }
   return hipGetLastError();
 }
 
