@@ -705,11 +705,7 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
         // plateau of exact 1.0f (tukey and partial tukeys) the product is the sample itself:
         // no load, and no multiply when the whole wave's span lies inside (bit-identical partials)
         const int32_t* wpl = a.wplat + 2 * ((size_t)fr.win * a.nwin + wi);
-#ifndef FRA_NOPLAT
         const bool plat = i0 >= wpl[0] && i0 + kChunk + MAXLAG <= wpl[1];
-#else
-        const bool plat = false && wpl;
-#endif
         float wcoef[kChunk + MAXLAG];
         if (plat) {
 #pragma unroll

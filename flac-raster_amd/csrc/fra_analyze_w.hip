@@ -492,7 +492,10 @@ template <int MAXLAG>
 #ifndef FRA_W_WAVES
 #define FRA_W_WAVES 5
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FRA_W_WAVES, 8)))
+#ifndef FRA_W_WAVES_MAX
+#define FRA_W_WAVES_MAX 8
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FRA_W_WAVES, FRA_W_WAVES_MAX)))
 k_analyze_w(JobArgs a, int src) {
   static_assert(MAXLAG == 8, "levels 3-6");
   __shared__ WaveSmem S;
