@@ -519,12 +519,23 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 #endif
 
 // One subframe by one workgroup: frame g, grid row cy (the channel, or for the 32-bit instance of a mid-side
-// stream the virtual channel cy + 2); rot rotates the wave roles; pf_allowed: the L2 prefetch may guess the
-// next workgroups by dispatch order (not in the redo-list mode)
+// stream the virtual channel cy + 2); rot rotates the wave roles.  List mode (beside k_analyze_w, the 16-bit lag-8
+// instance only): workgroup i takes entry i of the partial-subframe list (frame * 8 + channel), and the L2
+// prefetch -- which guesses later workgroups by dispatch order -- is off.  The body is the kernel itself: as a
+// device function taking the kernel arguments by reference it compiled to 125 instead of 101 VGPRs (32-bps
+// instance) and twice the SGPR spills.
 template <bool B32, int MAXLAG>
-__device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, const int g, const int cy, const int rot,
-                                           const bool pf_allowed) {
-  __shared__ AnalyzeSmem<B32, MAXLAG> S;  // (declared here, not passed by reference: keeps every access in LDS)
+__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
+  int g_ = a.frame_base + (int)blockIdx.x, c_ = (int)blockIdx.y;
+  if (!B32 && MAXLAG == 8 && a.redo) {
+    const int e = __builtin_amdgcn_readfirstlane(a.redo[blockIdx.x]);
+    g_ = e >> 3;
+    c_ = e & 7;
+  }
+  const int g = g_, cy = c_, rot = (int)((blockIdx.x + blockIdx.y) & 3);
+  const bool pf_allowed = B32 || MAXLAG != 8 || a.redo == nullptr;
+
+  __shared__ AnalyzeSmem<B32, MAXLAG> S;
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
   // wave index (and the wave role below) in SGPRs: a VGPR copy of them was spilled to scratch in the
   // 7-wave 16-bit instance
@@ -701,19 +712,11 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
           return;
         }
         // coefficients loaded here, not prefetched before the FIXED sums: a prefetch kept 16 + MAXLAG
-        // registers live through them and pushed the 7-wave instance into scratch.  Inside the window's
-        // plateau of exact 1.0f (tukey and partial tukeys) the product is the sample itself:
-        // no load, and no multiply when the whole wave's span lies inside (bit-identical partials)
-        const int32_t* wpl = a.wplat + 2 * ((size_t)fr.win * a.nwin + wi);
-        const bool plat = i0 >= wpl[0] && i0 + kChunk + MAXLAG <= wpl[1];
+        // registers live through them and pushed the 7-wave instance into scratch.  (No plateau skip of the
+        // exact-1.0 coefficients here, unlike k_analyze_w: its SGPR pressure cost more than the loads it saved,
+        // C5 117.0 -> 115.2 ms without it, profiles/r04_ab_plateau_k_analyze_c5.txt)
         float wcoef[kChunk + MAXLAG];
-        if (plat) {
-#pragma unroll
-          for (int j = 0; j < kChunk + MAXLAG; j++) wcoef[j] = 1.0f;
-        } else {
-          load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
-        }
-        const bool allplat = __all(plat);
+        load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];
@@ -725,7 +728,7 @@ __device__ __forceinline__ void analyze_wg(const JobArgs& a, const int src, cons
           for (int j = 0; j < kChunk + MAXLAG; j++) {
             const int i = i0 + j;
             const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
-            wf[j] = allplat ? (float)v : (float)v * wcoef[j];
+            wf[j] = (float)v * wcoef[j];
           }
         }
 
@@ -1475,19 +1478,6 @@ read_x28(S.smp, t, x);
   }
 }
 
-template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
-  // list mode (beside k_analyze_w): workgroup i takes entry i of the partial-subframe list (frame * 8 +
-  // channel); one call site, so the body is inlined once
-  int g = a.frame_base + (int)blockIdx.x, c = (int)blockIdx.y;
-  if (!B32 && MAXLAG == 8 && a.redo) {  // (only this instance runs beside k_analyze_w)
-    const int e = __builtin_amdgcn_readfirstlane(a.redo[blockIdx.x]);
-    g = e >> 3;
-    c = e & 7;
-  }
-  analyze_wg<B32, MAXLAG>(a, src, g, c, (int)((blockIdx.x + blockIdx.y) & 3),
-                          B32 || MAXLAG != 8 || a.redo == nullptr);
-}
 
 #ifdef FRA_STAMPS
 }  // namespace fra

@@ -524,13 +524,15 @@ k_analyze_w(JobArgs a, int src) {
   // ---- 1. load + normalise (table gather), OR / min / max
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+  // (the lambdas capture these locals, not the kernel arguments: taking the arguments' address costs registers)
+  const void* const raster = a.raster;
+  const int32_t* const lut = a.lut + (int64_t)fr.stream * a.lut_stride;
   auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx, bool first) {
-    const int32_t* lut = a.lut + (int64_t)fr.stream * a.lut_stride;
     switch (src) {  // wave-uniform
-      case ST_U8: wload_lut<ST_U8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      case ST_I8: wload_lut<ST_I8>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      case ST_U16: wload_lut<ST_U16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      default: wload_lut<ST_I16>(a.raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      case ST_U8: wload_lut<ST_U8>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      case ST_I8: wload_lut<ST_I8>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      case ST_U16: wload_lut<ST_U16>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
+      default: wload_lut<ST_I16>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
     }
   };
   load_samples(orv, vmin, vmax, true);
