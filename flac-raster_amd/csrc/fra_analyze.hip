@@ -527,13 +527,13 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
   int g_ = a.frame_base + (int)blockIdx.x, c_ = (int)blockIdx.y;
-  if (!B32 && MAXLAG == 8 && a.redo) {
-    const int e = __builtin_amdgcn_readfirstlane(a.redo[blockIdx.x]);
+  if (!B32 && MAXLAG == 8 && a.part) {
+    const int e = __builtin_amdgcn_readfirstlane(a.part[blockIdx.x]);
     g_ = e >> 3;
     c_ = e & 7;
   }
   const int g = g_, cy = c_, rot = (int)((blockIdx.x + blockIdx.y) & 3);
-  const bool pf_allowed = B32 || MAXLAG != 8 || a.redo == nullptr;
+  const bool pf_allowed = B32 || MAXLAG != 8 || a.part == nullptr;
 
   __shared__ AnalyzeSmem<B32, MAXLAG> S;
   constexpr int MAXO = MAXLAG > 4 ? MAXLAG : 4;  // predictor taps of the generic residual body
@@ -1503,8 +1503,8 @@ hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, i
                                hipStream_t s) {
   if (npart <= 0) return hipSuccess;
   JobArgs wa = a;
-  wa.redo = part;
-  wa.redo_n = npart;
+  wa.part = part;
+  wa.npart = npart;
   (void)max_part_blocks;
   k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, s>>>(wa, src);  // one workgroup per entry
   return hipGetLastError();
@@ -1524,8 +1524,8 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
     hipError_t e = hipSuccess;
     auto partial = [&](hipStream_t ps) {
       JobArgs wa = a;
-      wa.redo = part;
-      wa.redo_n = npart;
+      wa.part = part;
+      wa.npart = npart;
       k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
     };
     const bool fork = npart > 0 && side;

@@ -876,8 +876,8 @@ static void collect_times(fra_plan* p) {
 }
 
 // k_analyze_w (one subframe per wave, fra_analyze_w.hip) takes the full frames of 16-bit plans normalised
-// through the per-tile table with 8-byte sample vectors at levels 3-6 (handing back to k_analyze what it does
-// not finish); FRA_ANALYZE_WG=1 keeps every frame on the workgroup kernel (tests compare both)
+// through the per-tile table with 8-byte sample vectors at levels 3-6 (the partial frames' subframes go to
+// k_analyze as a list); FRA_ANALYZE_WG=1 keeps every frame on the workgroup kernel (tests compare both)
 static bool wave_path(const fra_plan* p) {
   const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
   return !wg && p->wave_ok && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&

@@ -209,8 +209,8 @@ struct JobArgs {
                            // (k_analyze fast load path: 32-bit lane offsets from a uniform base)
   int32_t frame_base;      // frame group of this launch (k_analyze / k_frame_scan / k_assemble):
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
-  const int32_t* redo;     // k_analyze list mode (beside k_analyze_w): (frame * 8 + channel) of the partial
-  int32_t redo_n;          //   subframes of the launch's frames, redo_n entries (null: the normal grid)
+  const int32_t* part;     // k_analyze list mode (beside k_analyze_w): (frame * 8 + channel) of the partial
+  int32_t npart;           //   subframes of the launch's frames, npart entries (null: the normal grid)
 };
 
 }  // namespace fra
