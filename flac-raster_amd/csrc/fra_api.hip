@@ -626,7 +626,8 @@ static int plan_build(fra_plan* p) {
     build_host_bands(p, nfr);
     // look-back words (zero: no tag yet) and tickets of every scan slot, sized for the whole plan
     const int nslot = (int)p->groups.size();
-    p->look_stride = std::max(256, frame_scan_blocks(nfr));  // (any group of <= nfr frames: <= 256 or nfr's count)
+    // any group of <= nfr frames needs <= 256 words by default, or nfr's count (one frame per thread when forced)
+    p->look_stride = std::max({256, frame_scan_blocks(nfr), (nfr + 255) / 256});
     HIPCHK(hipMalloc(&p->d_look, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
     HIPCHK(hipMemset(p->d_look, 0, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
     HIPCHK(hipMalloc(&p->d_ticket, sizeof(unsigned) * nslot));

@@ -21,6 +21,7 @@
 // is evaluated in exactly the order the oracle uses (IEEE add/mul/div are correctly rounded on
 // gfx950 and on x86-64, so identical op sequences give identical bits).
 #include <algorithm>
+#include <cstdlib>
 
 #include "fra_device.h"
 
@@ -399,7 +400,15 @@ hipError_t launch_minmax(int src, const JobArgs& a, int nstreams, int max_segs, 
 
 // frames per thread: one up to 65,536 frames (C4: 0.026 ms serial against 0.053 at four), then 4 / 16 so a
 // C5-size group stays at <= 256 workgroups beside the next execute's analysis
-static int scan_items(int nframes) { return nframes <= 65536 ? 1 : (nframes <= 4 * 65536 ? 4 : 16); }
+// (FRA_SCAN_ITEMS=1/4/16 forces one form for tests; it must be set before the plan is created, which sizes the
+// look-back words by it)
+static int scan_items(int nframes) {
+  if (const char* e = getenv("FRA_SCAN_ITEMS")) {
+    const int v = atoi(e);
+    if (v == 1 || v == 4 || v == 16) return v;
+  }
+  return nframes <= 65536 ? 1 : (nframes <= 4 * 65536 ? 4 : 16);
+}
 int frame_scan_blocks(int nframes) {
   const int per = 256 * scan_items(nframes);
   return (nframes + per - 1) / per;

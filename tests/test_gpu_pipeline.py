@@ -283,3 +283,16 @@ def test_host_raster_swap_between_pipelined_executes():
         assert plan.download()[1] == exp_b
     finally:
         plan.close()
+
+
+@pytest.mark.parametrize("items", ["1", "4", "16"])
+def test_frame_scan_forms_equal(monkeypatch, items):
+    """k_frame_scan's three forms (1, 4 or 16 frames per thread: the decoupled look-back over 1,024 / 256 / 64
+    workgroups of this plan) give the same offsets and bytes; FRA_SCAN_ITEMS is read when the plan is made."""
+    H, W = 9000, 8192  # 18,000 frames of one band: 71 / 18 / 5 workgroups (two look-back windows at 1)
+    r = synth_window(3, 17, 1, H, W)
+    wins = calculate_tiles(H, W, 512)
+    _, ref = N.encode_windows(r, wins, level=5, norm=16)
+    monkeypatch.setenv("FRA_SCAN_ITEMS", items)
+    infos, got = N.encode_windows(r, wins, level=5, norm=16)
+    assert got == ref
