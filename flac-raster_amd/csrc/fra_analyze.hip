@@ -66,15 +66,15 @@ __device__ unsigned long long g_fra_stamps[kStampWG * kStampN];
 template <bool B32>
 constexpr int buf_words() { return B32 ? kMaxBlock + 16 : kMaxBlock / 2 + 16; }
 
-// per-thread sample windows from the LDS array (chunk stride kSmpStride elements):
+// per-thread sample windows from the LDS array (chunk stride smp_stride<T>() elements):
 //   read_x28: x[j] = sample 16t - 12 + j (the previous chunk's last 12, the zero chunk for t = 0)
 //   read_y24: y[j] = sample 16t + j, j < 24 (this chunk + the next chunk's first 8)
 // int16 storage is read as aligned dword pairs and sign-extended (2 samples per ds_read lane-dword)
 __device__ __forceinline__ void read_x28(const int32_t* smp, int t, int32_t (&x)[28]) {
 #pragma unroll
-  for (int j = 0; j < 12; j++) x[j] = smp[t * kSmpStride + 4 + j];
+  for (int j = 0; j < 12; j++) x[j] = smp[t * smp_stride<int32_t>() + 4 + j];
 #pragma unroll
-  for (int j = 0; j < 16; j++) x[12 + j] = smp[(t + 1) * kSmpStride + j];
+  for (int j = 0; j < 16; j++) x[12 + j] = smp[(t + 1) * smp_stride<int32_t>() + j];
 }
 __device__ __forceinline__ void read_x28(const int16_t* smp, int t, int32_t (&x)[28]) {
   const uint32_t* d = reinterpret_cast<const uint32_t*>(smp);  // kSmpStride even: chunk starts dword-aligned
@@ -93,9 +93,9 @@ __device__ __forceinline__ void read_x28(const int16_t* smp, int t, int32_t (&x)
 }
 __device__ __forceinline__ void read_y24(const int32_t* smp, int t, int32_t (&y)[24]) {
 #pragma unroll
-  for (int j = 0; j < 16; j++) y[j] = smp[(t + 1) * kSmpStride + j];
+  for (int j = 0; j < 16; j++) y[j] = smp[(t + 1) * smp_stride<int32_t>() + j];
 #pragma unroll
-  for (int j = 0; j < 8; j++) y[16 + j] = smp[(t + 2) * kSmpStride + j];
+  for (int j = 0; j < 8; j++) y[16 + j] = smp[(t + 2) * smp_stride<int32_t>() + j];
 }
 __device__ __forceinline__ void read_y24(const int16_t* smp, int t, int32_t (&y)[24]) {
   const uint32_t* d = reinterpret_cast<const uint32_t*>(smp);
@@ -122,23 +122,33 @@ template <bool B32, int MAXLAG>
 struct AnalyzeSmem {
   // sample i at sidx(i); [0, kSmpStride) = zero chunk.  16-bit path: int16 (every sample fits), which
   // keeps the workgroup at <= 32 KiB LDS (5 workgroups per CU at 96 VGPRs)
-  typename std::conditional<B32, int32_t, int16_t>::type smp[kSmpWords];
+  using SmpT = typename std::conditional<B32, int32_t, int16_t>::type;
+  SmpT smp[smp_words<SmpT>()];
   // the encoded subframe (big-endian words, MSB first) is built in smp, dead once the winner's residuals
   // are in registers (32-bps: <= 40 KiB, 4 workgroups per CU instead of 3; 16-bit: <= 22.75 KiB)
   union {
     unsigned long long psum[kMaxModels][kMaxPart];  // reused as esum[kMaxPart][3] for the winner
+    // 32-bps: the autocorrelation partials and Levinson-Durbin rows live in the LPC models' sums, which are
+    // zeroed again once the models are quantised (32 KiB of LDS: 5 workgroups per CU)
+    struct {
+      unsigned long long fixed[5][kMaxPart];
+      double red[B32 ? kWinCap<MAXLAG>() : 1][4][MAXLAG + 1];
+      double lp[B32 ? kWinCap<MAXLAG>() : 1][MAXLAG > 0 ? lp_row(MAXLAG) : 1];
+    } ov;
   } u;
   int32_t warm[kMaxLpc];  // warm-up samples, saved before smp is reused as the bit buffer
-  union {
-    unsigned long long node[4][2 * kMaxPart];  // per-wave partition-tree node sums, level p at [2^p, 2^(p+1))
-    struct {  // after the model search (node is dead): winner's exact-pass sums / Rice parameters
+  union {  // (a union of one since the partition search left LDS)
+    struct {  // after the model search: winner's exact-pass sums / Rice parameters
       unsigned long long esum2[kMaxPart][3];  // fast frames: sums of u >> (k0-1), u >> k0, u >> (k0+1)
       int32_t kpart[kMaxPart];
       int32_t kfin[kMaxPart];
     } e;
   } nu;
-  double red[kWinCap<MAXLAG>()][4][MAXLAG + 1];  // per window, per wave: reduced chunk partials
-  double lp[kWinCap<MAXLAG>()][MAXLAG > 0 ? lp_row(MAXLAG) : 1];  // LD rows per window (triangular)
+  // 16-bit instances: per window, per wave: reduced chunk partials; LD rows per window (triangular)
+  double red_[B32 ? 1 : kWinCap<MAXLAG>()][4][MAXLAG + 1];
+  double lp_[B32 ? 1 : kWinCap<MAXLAG>()][MAXLAG > 0 ? lp_row(MAXLAG) : 1];
+  __device__ auto& red() { if constexpr (B32) return u.ov.red; else return red_; }
+  __device__ auto& lp() { if constexpr (B32) return u.ov.lp; else return lp_; }
   // model table in the narrowest types (16-bit path: 7 workgroups per CU need <= 22.5 KiB of LDS):
   // qlp coefficients < 2^15, orders/shifts/partition orders < 128
   int16_t mcoef[kMaxModels][kMaxLpc];
@@ -327,160 +337,15 @@ __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kM
   g2 = __builtin_amdgcn_readfirstlane(h2);
 }
 
-// porder_search (below) when every node sum is < 2^29: the same nodes, tree, tie rule and outputs in
-// 32-bit arithmetic (one-instruction DPP adds, rice_pick32)
-__device__ __forceinline__ void porder_search32(const unsigned long long* psum, uint32_t* node, int P, int pm, int n,
-                                                int o, int lane, uint32_t Sv, uint64_t& best_out, int& bp_out,
-                                                uint8_t* kout) {
-  (void)psum;
-  if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
-#define FRA_NODE_STEP32(S_)                                                        \
-  if (P > S_) {                                                                    \
-    Sv = up_add32<S_>(Sv);                                                         \
-    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
-      node[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = Sv;                         \
-  }
-  FRA_NODE_STEP32(0)
-  FRA_NODE_STEP32(1)
-  FRA_NODE_STEP32(2)
-  FRA_NODE_STEP32(3)
-  FRA_NODE_STEP32(4)
-  FRA_NODE_STEP32(5)
-#undef FRA_NODE_STEP32
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-  uint32_t bits32 = 0;
-  bool big = false;
-  const int p = lane ? 31 - __clz(lane) : 0;
-  int kn = 0;
-  if (lane >= 1 && p <= P && p <= pm) {
-    const int j = lane - (1 << p);
-    rice_pick32((uint32_t)((n >> p) - (j == 0 ? o : 0)), node[lane], kn, bits32);
-    big = kn > 14;
-  }
-  const uint64_t bigm = __ballot(big);
-  uint32_t tot[7];
-  uint32_t v = bits32;
-  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-  v += dpp32<DPP_SHR1, 0xF>(v);
-  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
-  v += dpp32<DPP_SHR2, 0xF>(v);
-  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
-  v += dpp32<DPP_SHR4, 0xF>(v);
-  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-  v += dpp32<DPP_SHR8, 0xF>(v);
-  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-  v += dpp32<DPP_BC15, 0xA>(v);
-  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-  tot[6] = 0;
-  bool big6 = false;
-  int k6 = 0;
-  if (P == 6 && pm == 6) {  // level 6: 64 nodes at node[64 + lane]
-    uint32_t b6;
-    rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), node[64 + lane], k6, b6);
-    tot[6] = wave_sum32(b6);
-    big6 = __any(k6 > 14);
-  }
-  uint64_t best = 0;
-  int bp = pm;
-  for (int q = pm; q >= 0; q--) {
-    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
-    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
-    if (q == pm || t <= best) { best = t; bp = q; }
-  }
-  best_out = best;
-  bp_out = bp;
-  if (kout) {
-    if (bp == 6) kout[lane] = (uint8_t)k6;
-    else if (lane >= (1 << bp) && lane < (2 << bp)) kout[lane - (1 << bp)] = (uint8_t)kn;
-  }
-}
-
-// Evaluate every node of one model's partition tree (one wave).  Node (level p, index j) lives at
-// lane 2^p + j (level P = 6 nodes in a second register), so each lane runs ONE Rice estimate and
-// the per-level totals come out of a single upper-lane DPP chain (level p's segment is the aligned
-// lane group [2^p, 2^(p+1)), summed after p steps) and one ballot.  Same totals and tie rule as the
-// oracle's per-level loop (iterate p = pm..0, keep '<=').
-__device__ __forceinline__ void porder_search(const unsigned long long* psum, unsigned long long* node, int P, int pm,
-                                              int n, int o, int lane, uint64_t& best_out, int& bp_out,
-                                              uint8_t* kout = nullptr) {
-  // node sums: finest sums S_j, then upper-lane group sums (leader lane of 2^s lanes = (j+1)2^s - 1)
-  uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
-  if (__all(Sv < (1ull << 23))) {
-    // every node sum < 2^29 (<= 64 finest partitions of < 2^23): the whole search in 32-bit arithmetic
-    // (rice_pick32), bit-identical to the 64-bit form below; node sums kept as u32 in the same buffer
-    porder_search32(psum, reinterpret_cast<uint32_t*>(node), P, pm, n, o, lane, (uint32_t)Sv, best_out, bp_out, kout);
-    return;
-  }
-  if (lane < (1 << P)) node[(1 << P) + lane] = Sv;
-#define FRA_NODE_STEP(S_)                                                          \
-  if (P > S_) {                                                                    \
-    Sv = up_add64<S_>(Sv);                                                         \
-    if (lane < (1 << P) && ((lane + 1) & ((2 << S_) - 1)) == 0)                    \
-      node[(1 << (P - S_ - 1)) + (lane >> (S_ + 1))] = Sv;                         \
-  }
-  FRA_NODE_STEP(0)
-  FRA_NODE_STEP(1)
-  FRA_NODE_STEP(2)
-  FRA_NODE_STEP(3)
-  FRA_NODE_STEP(4)
-  FRA_NODE_STEP(5)
-#undef FRA_NODE_STEP
-  // this wave's node stores -> its own reads (DS ops of one wave complete in order)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-  // levels 0..min(P,5): lane = 2^p + j
-  uint32_t bits32 = 0;
-  bool big = false;
-  const int p = lane ? 31 - __clz(lane) : 0;
-  int kn = 0;
-  if (lane >= 1 && p <= P && p <= pm) {
-    const int j = lane - (1 << p);
-    const uint64_t cnt = (uint64_t)((n >> p) - (j == 0 ? o : 0));
-    uint64_t bits;
-    rice_pick(cnt, node[lane], kn, bits);
-    bits32 = (uint32_t)bits;
-    big = kn > 14;
-  }
-  const uint64_t bigm = __ballot(big);
-  uint32_t tot[7];
-  uint32_t v = bits32;
-  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-  v += dpp32<DPP_SHR1, 0xF>(v);
-  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
-  v += dpp32<DPP_SHR2, 0xF>(v);
-  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
-  v += dpp32<DPP_SHR4, 0xF>(v);
-  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-  v += dpp32<DPP_SHR8, 0xF>(v);
-  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-  v += dpp32<DPP_BC15, 0xA>(v);
-  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-  tot[6] = 0;
-  bool big6 = false;
-  int k6 = 0;
-  if (P == 6 && pm == 6) {  // level 6: 64 nodes at node[64 + lane]
-    const uint64_t cnt = (uint64_t)((n >> 6) - (lane == 0 ? o : 0));
-    uint64_t bits;
-    rice_pick(cnt, node[64 + lane], k6, bits);
-    tot[6] = wave_sum32((uint32_t)bits);
-    big6 = __any(k6 > 14);
-  }
-  uint64_t best = 0;
-  int bp = pm;
-  for (int q = pm; q >= 0; q--) {
-    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
-    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
-    if (q == pm || t <= best) { best = t; bp = q; }
-  }
-  best_out = best;
-  bp_out = bp;
-  if (kout) {  // the chosen order's per-partition estimates (node (bp, j) at lane 2^bp + j)
-    if (bp == 6) kout[lane] = (uint8_t)k6;
-    else if (lane >= (1 << bp) && lane < (2 << bp)) kout[lane - (1 << bp)] = (uint8_t)kn;
-  }
+// Every partition order of one model's finest sums psum[0, 2^P) in one wave (porder_search_reg,
+// fra_device.h: node sums by the upper-lane DPP tree and ds_bpermute, no LDS); kout[j], j < 2^bp, receives
+// partition j's Rice parameter at the chosen order
+__device__ __forceinline__ void porder_search(const unsigned long long* psum, int P, int pm, int n, int o, int lane,
+                                              uint64_t& best_out, int& bp_out, uint8_t* kout = nullptr) {
+  const uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
+  uint32_t kreg = 0;
+  porder_search_reg(Sv, P, pm, n, o, lane, best_out, bp_out, kreg);
+  if (kout && (bp_out == 6 || lane < (1 << bp_out))) kout[lane] = (uint8_t)kreg;
 }
 
 // VERBATIM subframe written word by word straight to its slot (32-bps path, whose LDS bit buffer aliases
@@ -496,7 +361,7 @@ __device__ __forceinline__ uint32_t verbatim_word(const SmpT* smp, int n, uint32
   for (int s = s0; s < n && (int64_t)hdr + (int64_t)s * sbps < wb + 32; s++) {
     const int64_t rel = (int64_t)hdr + (int64_t)s * sbps - wb;
     const int sft = 32 - (int)rel - sbps;
-    const uint64_t v = (uint64_t)((uint32_t)smp[sidx(s)] & smask);
+    const uint64_t v = (uint64_t)((uint32_t)smp[sidx(smp, s)] & smask);
     word |= sft >= 0 ? (uint32_t)(v << sft) : (uint32_t)(v >> -sft);
   }
   return word;
@@ -525,7 +390,7 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 // device function taking the kernel arguments by reference it compiled to 125 instead of 101 VGPRs (32-bps
 // instance) and twice the SGPR spills.
 template <bool B32, int MAXLAG>
-__global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
+__global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
   int g_ = a.frame_base + (int)blockIdx.x, c_ = (int)blockIdx.y;
   if (!B32 && MAXLAG == 8 && a.part) {
     const int e = __builtin_amdgcn_readfirstlane(a.part[blockIdx.x]);
@@ -570,7 +435,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
   // ---- 1. load + normalise
   uint32_t pf = 0u;  // prefetch words (FRA_PREFETCH), consumed at the end of the fast path
   bool pf_ok = false;
-  if (t < kSmpStride) S.smp[t] = 0;  // zero chunk (samples before the block start)
+  if (t < smp_stride<typename AnalyzeSmem<B32, MAXLAG>::SmpT>()) S.smp[t] = 0;  // zero chunk (samples before the block start)
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   {
@@ -621,7 +486,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
   const int w = __builtin_ctz(orv);
   const int sbps = bps - w;
   if (w) {
-    for (int i = t; i < n; i += kThreads) S.smp[sidx(i)] = S.smp[sidx(i)] >> w;
+    for (int i = t; i < n; i += kThreads) S.smp[sidx(S.smp, i)] = S.smp[sidx(S.smp, i)] >> w;
     __syncthreads();
   }
   const uint32_t hdr = 8u + (uint32_t)(w ? w : 0);
@@ -708,7 +573,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
       // at their first use.
       auto window_acf = [&](const int wi, const bool act) {
         if (!act) {
-          if (lane <= MAXLAG) S.red[wi][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
+          if (lane <= MAXLAG) S.red()[wi][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
           return;
         }
         // coefficients loaded here, not prefetched before the FIXED sums: a prefetch kept 16 + MAXLAG
@@ -727,7 +592,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
 #pragma unroll
           for (int j = 0; j < kChunk + MAXLAG; j++) {
             const int i = i0 + j;
-            const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(min(i, kMaxBlock - 1))];
+            const int32_t v = j < kChunk + 8 ? y[j] : S.smp[sidx(S.smp, min(i, kMaxBlock - 1))];
             wf[j] = (float)v * wcoef[j];
           }
         }
@@ -751,7 +616,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
         double acc[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++) acc[l] = (double)(pacc[l].x + pacc[l].y);
-        autocorr_reduce_wave<MAXLAG + 1>(acc, S.red[wi][wv], lane);
+        autocorr_reduce_wave<MAXLAG + 1>(acc, S.red()[wi][wv], lane);
       };
       for (int wi = 0; wi < a.nwin; wi++) window_acf(wi, wave_active(wi));
       __syncthreads();
@@ -778,7 +643,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
           const int pm = max_porder(n, m, cfg.max_porder);
           uint64_t best = 0;
           int bp = pm;
-          porder_search(S.u.psum[m], S.nu.node[rw], P, pm, n, m, lane, best, bp, S.kbest[m]);
+          porder_search(S.u.psum[m], P, pm, n, m, lane, best, bp, S.kbest[m]);
           if (lane == 0) {
             S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
             S.mporder[m] = bp;
@@ -794,10 +659,10 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
         double ac[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++)
-          ac[l] = l <= lmax ? (S.red[ws][0][l] + S.red[ws][1][l]) + (S.red[ws][2][l] + S.red[ws][3][l]) : 0.0;
+          ac[l] = l <= lmax ? (S.red()[ws][0][l] + S.red()[ws][1][l]) + (S.red()[ws][2][l] + S.red()[ws][3][l]) : 0.0;
         int nord = 0;
         double errv[MAXLAG];
-        if (gon && ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp[ws], errv, lo == 0);
+        if (gon && ac[0] != 0.0) nord = levinson_wave<MAXLAG>(ac, lmax, S.lp()[ws], errv, lo == 0);
         double e = errv[0];
 #pragma unroll
         for (int j = 1; j < MAXLAG; j++)
@@ -824,7 +689,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
           o = (int)__builtin_ctz(rowbits);
           double lpo[MAXLAG];
 #pragma unroll
-          for (int j = 0; j < MAXLAG; j++) lpo[j] = j < o ? -S.lp[ws][lp_row(o - 1) + j] : 0.0;  // lp = -lpc
+          for (int j = 0; j < MAXLAG; j++) lpo[j] = j < o ? -S.lp()[ws][lp_row(o - 1) + j] : 0.0;  // lp = -lpc
           ok = quantize<MAXLAG>(lpo, o, prec, q, sh);
         }
         if (gon && lo == 0) {
@@ -848,6 +713,10 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
   else if (fastframe) read_d14(S.smp, t, D);
   else read_x28(S.smp, t, x);
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
+  if constexpr (B32) {  // the LPC models' sums held the autocorrelation / LD rows: zero them again
+    for (int i = t; i < (kMaxModels - 5) * kMaxPart; i += kThreads) (&S.u.psum[5][0])[i] = 0ull;
+    __syncthreads();
+  }
   FRA_STAMP(4)
   double xd[B32 ? 12 + kChunk : 1];  // 32-bps fast path: x as exact doubles
   if (fastframe) {
@@ -946,15 +815,14 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], S.nu.node[rw], P, pm, n, o, lane, best, bp, S.kbest[m]);
+    porder_search(S.u.psum[m], P, pm, n, o, lane, best, bp, S.kbest[m]);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
     }
     FRA_ROLE_STAMP(18)
   }
-  {  // esum2 aliases node[0..1], dead once this wave's searches are done: zero this wave's share
-    static_assert(kMaxPart * 3 <= 2 * (2 * kMaxPart), "esum2 inside node[0..1]");
+  {  // zero the winner's exact-pass sums (waves 0 and 1 share the 3 x kMaxPart words)
     unsigned long long* ez = &S.nu.e.esum2[0][0];
     const int e1 = min(kMaxPart * 3, (rw + 1) * 2 * kMaxPart);
     for (int i = rw * 2 * kMaxPart + lane; i < e1; i += 64) ez[i] = 0ull;
@@ -1043,7 +911,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 4 : (MAXLAG > 8 ? 4 : kWaves16
         for (int jj = 0; jj < 12; jj++)
           if (jj < o) uu[jj] = 0u;
       }
-      if (t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the next barrier
+      if (t < o) S.warm[t] = S.smp[sidx(S.smp, t)];  // smp becomes the bit buffer after the next barrier
       // 16-bit: u < 2^28, so 16 of them fit 32 bits; 32-bps: 64-bit partial sums
       typename std::conditional<B32, uint64_t, uint32_t>::type fs0 = 0, fs1 = 0, fs2 = 0;
       {
@@ -1277,7 +1145,7 @@ read_x28(S.smp, t, x);
       uu[jj] = (i < n && i >= o) ? uv : 0u;
     }
   }
-  if (t < o) S.warm[t] = S.smp[sidx(t)];  // smp becomes the bit buffer after the decision
+  if (t < o) S.warm[t] = S.smp[sidx(S.smp, t)];  // smp becomes the bit buffer after the decision
   __syncthreads();
   {
     const int pz = n >> ps;

@@ -70,12 +70,6 @@ __device__ __forceinline__ void wread_d14(const uint32_t* sw, int lane, int j, u
   D[6] = o0.x; D[7] = o0.y; D[8] = o0.z; D[9] = o0.w;
   D[10] = o1.x; D[11] = o1.y; D[12] = o1.z; D[13] = o1.w;
 }
-__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src) {  // lane src's v (ds_bpermute)
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
-}
-__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src) {
-  return ((uint64_t)bperm32((uint32_t)(v >> 32), src) << 32) | bperm32((uint32_t)v, src);
-}
 __device__ __forceinline__ void unpack28(const uint32_t (&D)[14], int32_t (&x)[28]) {
 #pragma unroll
   for (int k = 0; k < 14; k++) {
@@ -232,151 +226,6 @@ __device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, i
   g1 = __builtin_amdgcn_readfirstlane(h1);
   g2 = __builtin_amdgcn_readfirstlane(h2);
 }
-
-// porder_search (fra_analyze.hip) on a register of finest partition sums (lane p < 2^P), without LDS: node
-// (level q, index j) -- the sum of finest partitions [j 2^(P-q), (j+1) 2^(P-q)) -- is needed at lane 2^q + j;
-// the upper-lane tree leaves it after step P - q - 1 at lane (j+1) 2^(P-q) - 1, one ds_bpermute per step.
-// Same nodes, tree, tie rule and outputs as porder_search; kreg lane j < 2^bp = partition j's Rice parameter
-__device__ __forceinline__ void porder_search_w(uint64_t Sv, int P, int pm, int n, int o, int lane, uint64_t& best_out,
-                                                int& bp_out, uint32_t& kreg) {
-  const int p = lane ? 31 - __clz(lane) : 0;  // this lane's level; j = lane - 2^p
-  const int jn = lane - (1 << p);
-  uint32_t bits32 = 0;
-  bool big = false;
-  int kn = 0;
-  uint32_t tot6 = 0;
-  bool big6 = false;
-  int k6 = 0;
-  if (__all(Sv < (1ull << 23))) {  // every node sum < 2^29: 32-bit arithmetic (rice_pick32), bit-identical
-    uint32_t S = (uint32_t)Sv;
-    // level P <= 5: the finest sums themselves (every ds_bpermute runs on all 64 lanes: a source lane outside
-    // EXEC would read as 0, so none may sit under a lane-dependent condition)
-    const uint32_t fin = bperm32(S, jn & 63);
-    uint32_t nv = p == P ? fin : 0u;
-#define FRA_NODE_STEP32(S_)                                                        \
-  if (P > S_) {                                                                    \
-    S = up_add32<S_>(S);                                                           \
-    const uint32_t tv = bperm32(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
-    nv = p == P - S_ - 1 ? tv : nv;                                                \
-  }
-    FRA_NODE_STEP32(0) FRA_NODE_STEP32(1) FRA_NODE_STEP32(2)
-    FRA_NODE_STEP32(3) FRA_NODE_STEP32(4) FRA_NODE_STEP32(5)
-#undef FRA_NODE_STEP32
-    if (lane >= 1 && p <= P && p <= pm) {
-      rice_pick32((uint32_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits32);
-      big = kn > 14;
-    }
-    if (P == 6 && pm == 6) {  // level 6: the finest sums at lane j
-      uint32_t b6;
-      rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), (uint32_t)Sv, k6, b6);
-      tot6 = wave_sum32(b6);
-      big6 = __any(k6 > 14);
-    }
-  } else {
-    uint64_t S = Sv;
-    const uint64_t fin = bperm64(S, jn & 63);
-    uint64_t nv = p == P ? fin : 0ull;
-#define FRA_NODE_STEP(S_)                                                          \
-  if (P > S_) {                                                                    \
-    S = up_add64<S_>(S);                                                           \
-    const uint64_t tv = bperm64(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
-    nv = p == P - S_ - 1 ? tv : nv;                                                \
-  }
-    FRA_NODE_STEP(0) FRA_NODE_STEP(1) FRA_NODE_STEP(2)
-    FRA_NODE_STEP(3) FRA_NODE_STEP(4) FRA_NODE_STEP(5)
-#undef FRA_NODE_STEP
-    if (lane >= 1 && p <= P && p <= pm) {
-      uint64_t bits;
-      rice_pick((uint64_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits);
-      bits32 = (uint32_t)bits;
-      big = kn > 14;
-    }
-    if (P == 6 && pm == 6) {
-      uint64_t b6;
-      rice_pick((uint64_t)((n >> 6) - (lane == 0 ? o : 0)), Sv, k6, b6);
-      tot6 = wave_sum32((uint32_t)b6);
-      big6 = __any(k6 > 14);
-    }
-  }
-  const uint64_t bigm = __ballot(big);
-  uint32_t tot[7];
-  uint32_t v = bits32;
-  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-  v += dpp32<DPP_SHR1, 0xF>(v);
-  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
-  v += dpp32<DPP_SHR2, 0xF>(v);
-  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
-  v += dpp32<DPP_SHR4, 0xF>(v);
-  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-  v += dpp32<DPP_SHR8, 0xF>(v);
-  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-  v += dpp32<DPP_BC15, 0xA>(v);
-  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-  tot[6] = tot6;
-  uint64_t best = 0;
-  int bp = pm;
-  for (int q = pm; q >= 0; q--) {
-    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
-    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
-    if (q == pm || t <= best) { best = t; bp = q; }
-  }
-  best_out = best;
-  bp_out = bp;
-  // partition j's parameter at order bp: node (bp, j) sits at lane 2^bp + j (level 6: k6 at lane j)
-  const int kl = __shfl(kn, ((1 << (bp < 6 ? bp : 0)) + lane) & 63, 64);
-  kreg = (uint32_t)(bp == 6 ? k6 : kl);
-}
-
-#ifdef FRA_STAMPS
-// diagnostic build only (csrc/Makefile `wstamps`, tools/wstamp_phases.py): lane 0 of the first kWStampW waves
-// stores s_memtime after each phase, inside the real steady state
-constexpr unsigned kWStampW = 1u << 18, kWStampN = 16;
-__device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
-#define FRA_WSTAMP(k)                                                                            \
-  if (lane == 0) {                                                                               \
-    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
-    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = __builtin_amdgcn_s_memtime();      \
-  }
-#define FRA_WSTAMP_VAL(k, v)                                                                     \
-  if (lane == 0) {                                                                               \
-    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
-    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = (unsigned long long)(v);            \
-  }
-// FRA_WSTAMP_FINE: the load phase split at forced waits (metadata, raw rows, LUT gathers + LDS stores)
-#ifdef FRA_WSTAMP_FINE
-#define FRA_WSTAMP_WAIT(k)                                      \
-  {                                                             \
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-    FRA_WSTAMP(k)                                               \
-  }
-#endif
-#endif
-#ifndef FRA_WSTAMP
-#define FRA_WSTAMP(k)
-#define FRA_WSTAMP_VAL(k, v)
-#endif
-#ifndef FRA_WSTAMP_WAIT
-#define FRA_WSTAMP_WAIT(k) {}
-#endif
-// phase-stop diagnostic builds (csrc/Makefile `wstops`, tools/pmc_stall_phases.sh): every subframe is first
-// described as VERBATIM (valid sizes: the frame scan and the assembly stay inside their buffers; the bytes
-// are meaningless), then the wave returns after phase k, keeping that phase's results alive through the
-// descriptor's unused cval
-#ifdef FRA_WSTOP
-#define FRA_WSTOP_AT(k, keep)                      \
-  if (FRA_WSTOP == (k)) {                          \
-    if (lane == 0) d->cval = (int32_t)(keep);      \
-    return;                                        \
-  }
-#define FRA_WSTOP_AT_T(k, keep)                    \
-  if (FRA_WSTOP == (k)) {                          \
-    if (lane == 0) d->cval = (int32_t)(keep);      \
-    return true;                                   \
-  }
-#else
-#define FRA_WSTOP_AT(k, keep)
-#define FRA_WSTOP_AT_T(k, keep)
-#endif
 
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
 // lane l loads the 8-byte vectors l + 64k (all issued before the first use), gathers each sample's audio
@@ -898,7 +747,7 @@ k_analyze_w(JobArgs a, int src) {
     uint64_t best;
     int bp;
     uint32_t kreg;
-    porder_search_w(psum, P, pm, n, o, lane, best, bp, kreg);
+    porder_search_reg(psum, P, pm, n, o, lane, best, bp, kreg);
     const uint64_t est = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + best;
     offer((uint32_t)est, m, type, o, sh, qm, bp, kreg);
   }

@@ -218,16 +218,16 @@ __device__ __forceinline__ void load_mid_side_t(const void* base, const StreamDe
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int i = sidx_of(k);
-    if (i < n) smp[sidx(i)] = audio(raw[k]);
+    if (i < n) smp[sidx(smp, i)] = audio(raw[k]);
   }
   load_raw_t<SRC, VEC, int32_t>(base, st, fr, 1, raw);
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int i = sidx_of(k);
     if (i < n) {
-      const int32_t l = smp[sidx(i)], r = audio(raw[k]);
+      const int32_t l = smp[sidx(smp, i)], r = audio(raw[k]);
       const int32_t v = msmode == 1 ? ((l + r) >> 1) : l - r;
-      smp[sidx(i)] = v;
+      smp[sidx(smp, i)] = v;
       orv |= (uint32_t)v;
       vmin = min(vmin, v);
       vmax = max(vmax, v);
@@ -265,7 +265,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       for (int k = 0; k < K; k++) {
         const int i = sidx_of(k);
         if (i < n) {
-          smp[sidx(i)] = (SmpT)v[k];
+          smp[sidx(smp, i)] = (SmpT)v[k];
           orv |= (uint32_t)v[k];
           vmin = min(vmin, v[k]);
           vmax = max(vmax, v[k]);
@@ -281,7 +281,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
       int32_t v;
       if (np.mode == 0) v = (int32_t)raw[k];
       else v = norm_sample<SRC>((double)raw[k], np);
-      smp[sidx(i)] = (SmpT)v;
+      smp[sidx(smp, i)] = (SmpT)v;
       orv |= (uint32_t)v;
       vmin = min(vmin, v);
       vmax = max(vmax, v);
@@ -342,7 +342,7 @@ __device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDe
     for (int h = 0; h < V / 4; h++) {
       const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)g[kv * V + 4 * h + 1], (uint32_t)g[kv * V + 4 * h], 0x05040100u);
       const uint32_t p1 = __builtin_amdgcn_perm((uint32_t)g[kv * V + 4 * h + 3], (uint32_t)g[kv * V + 4 * h + 2], 0x05040100u);
-      *reinterpret_cast<uint2*>(smp + sidx(i + 4 * h)) = make_uint2(p0, p1);
+      *reinterpret_cast<uint2*>(smp + sidx(smp, i + 4 * h)) = make_uint2(p0, p1);
       orp |= p0 | p1;
       const i16x2 a0 = __builtin_bit_cast(i16x2, p0), a1 = __builtin_bit_cast(i16x2, p1);
       pmin = __builtin_elementwise_min(pmin, __builtin_elementwise_min(a0, a1));
@@ -869,12 +869,12 @@ template <bool B32, int MAXO, typename SmpT>
 __device__ __forceinline__ int64_t gres_lds(const SmpT* smp, int i, const int32_t* q, int sh) {
   if constexpr (B32) {
     int64_t sum = 0;
-    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[sidx(max(0, i - 1 - j))];
-    return (int64_t)smp[sidx(i)] - (sum >> sh);
+    for (int j = 0; j < MAXO; j++) sum += (int64_t)q[j] * (int64_t)smp[sidx(smp, max(0, i - 1 - j))];
+    return (int64_t)smp[sidx(smp, i)] - (sum >> sh);
   } else {
     int32_t sum = 0;
-    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], (int32_t)smp[sidx(max(0, i - 1 - j))]);
-    return (int64_t)((int32_t)smp[sidx(i)] - (sum >> sh));
+    for (int j = 0; j < MAXO; j++) sum += __mul24(q[j], (int32_t)smp[sidx(smp, max(0, i - 1 - j))]);
+    return (int64_t)((int32_t)smp[sidx(smp, i)] - (sum >> sh));
   }
 }
 
@@ -979,6 +979,160 @@ __device__ __forceinline__ uint32_t prefetch_rows(const JobArgs& a, int lane) {
   const uint32_t c0 = (uint32_t)f2.col0 + 64u * (uint32_t)lane;
   return word(c0) ^ word(c0 + 63u);
 }
+
+// ---------------------------------------------------------------- cross-lane gathers and the partition search
+__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src) {  // lane src's v (ds_bpermute)
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src) {
+  return ((uint64_t)bperm32((uint32_t)(v >> 32), src) << 32) | bperm32((uint32_t)v, src);
+}
+
+// Partition-order search (FRA-1 3.8) on a register of finest partition sums (lane p < 2^P), without LDS: node
+// (level q, index j) -- the sum of finest partitions [j 2^(P-q), (j+1) 2^(P-q)) -- is needed at lane 2^q + j;
+// the upper-lane tree leaves it after step P - q - 1 at lane (j+1) 2^(P-q) - 1, one ds_bpermute per step.
+// Same nodes, tree, tie rule and outputs as the oracle's per-level loop (p = pm..0, keep '<='); every node sum
+// < 2^29 runs in 32-bit arithmetic (rice_pick32, bit-identical); kreg lane j < 2^bp = partition j's Rice parameter
+__device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, int n, int o, int lane, uint64_t& best_out,
+                                                int& bp_out, uint32_t& kreg) {
+  const int p = lane ? 31 - __clz(lane) : 0;  // this lane's level; j = lane - 2^p
+  const int jn = lane - (1 << p);
+  uint32_t bits32 = 0;
+  bool big = false;
+  int kn = 0;
+  uint32_t tot6 = 0;
+  bool big6 = false;
+  int k6 = 0;
+  if (__all(Sv < (1ull << 23))) {  // every node sum < 2^29: 32-bit arithmetic (rice_pick32), bit-identical
+    uint32_t S = (uint32_t)Sv;
+    // level P <= 5: the finest sums themselves (every ds_bpermute runs on all 64 lanes: a source lane outside
+    // EXEC would read as 0, so none may sit under a lane-dependent condition)
+    const uint32_t fin = bperm32(S, jn & 63);
+    uint32_t nv = p == P ? fin : 0u;
+#define FRA_NODE_STEP32(S_)                                                        \
+  if (P > S_) {                                                                    \
+    S = up_add32<S_>(S);                                                           \
+    const uint32_t tv = bperm32(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
+    nv = p == P - S_ - 1 ? tv : nv;                                                \
+  }
+    FRA_NODE_STEP32(0) FRA_NODE_STEP32(1) FRA_NODE_STEP32(2)
+    FRA_NODE_STEP32(3) FRA_NODE_STEP32(4) FRA_NODE_STEP32(5)
+#undef FRA_NODE_STEP32
+    if (lane >= 1 && p <= P && p <= pm) {
+      rice_pick32((uint32_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits32);
+      big = kn > 14;
+    }
+    if (P == 6 && pm == 6) {  // level 6: the finest sums at lane j
+      uint32_t b6;
+      rice_pick32((uint32_t)((n >> 6) - (lane == 0 ? o : 0)), (uint32_t)Sv, k6, b6);
+      tot6 = wave_sum32(b6);
+      big6 = __any(k6 > 14);
+    }
+  } else {
+    uint64_t S = Sv;
+    const uint64_t fin = bperm64(S, jn & 63);
+    uint64_t nv = p == P ? fin : 0ull;
+#define FRA_NODE_STEP(S_)                                                          \
+  if (P > S_) {                                                                    \
+    S = up_add64<S_>(S);                                                           \
+    const uint64_t tv = bperm64(S, (((jn + 1) << (S_ + 1)) - 1) & 63);             \
+    nv = p == P - S_ - 1 ? tv : nv;                                                \
+  }
+    FRA_NODE_STEP(0) FRA_NODE_STEP(1) FRA_NODE_STEP(2)
+    FRA_NODE_STEP(3) FRA_NODE_STEP(4) FRA_NODE_STEP(5)
+#undef FRA_NODE_STEP
+    if (lane >= 1 && p <= P && p <= pm) {
+      uint64_t bits;
+      rice_pick((uint64_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits);
+      bits32 = (uint32_t)bits;
+      big = kn > 14;
+    }
+    if (P == 6 && pm == 6) {
+      uint64_t b6;
+      rice_pick((uint64_t)((n >> 6) - (lane == 0 ? o : 0)), Sv, k6, b6);
+      tot6 = wave_sum32((uint32_t)b6);
+      big6 = __any(k6 > 14);
+    }
+  }
+  const uint64_t bigm = __ballot(big);
+  uint32_t tot[7];
+  uint32_t v = bits32;
+  tot[0] = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
+  v += dpp32<DPP_SHR1, 0xF>(v);
+  tot[1] = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+  v += dpp32<DPP_SHR2, 0xF>(v);
+  tot[2] = (uint32_t)__builtin_amdgcn_readlane((int)v, 7);
+  v += dpp32<DPP_SHR4, 0xF>(v);
+  tot[3] = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  v += dpp32<DPP_SHR8, 0xF>(v);
+  tot[4] = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  v += dpp32<DPP_BC15, 0xA>(v);
+  tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  tot[6] = tot6;
+  uint64_t best = 0;
+  int bp = pm;
+  for (int q = pm; q >= 0; q--) {
+    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
+    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
+    if (q == pm || t <= best) { best = t; bp = q; }
+  }
+  best_out = best;
+  bp_out = bp;
+  // partition j's parameter at order bp: node (bp, j) sits at lane 2^bp + j (level 6: k6 at lane j)
+  const int kl = __shfl(kn, ((1 << (bp < 6 ? bp : 0)) + lane) & 63, 64);
+  kreg = (uint32_t)(bp == 6 ? k6 : kl);
+}
+
+#ifdef FRA_STAMPS
+// diagnostic build only (csrc/Makefile `wstamps`, tools/wstamp_phases.py): lane 0 of the first kWStampW waves
+// stores s_memtime after each phase, inside the real steady state
+constexpr unsigned kWStampW = 1u << 18, kWStampN = 16;
+__device__ unsigned long long g_fra_wstamps[kWStampW * kWStampN];
+#define FRA_WSTAMP(k)                                                                            \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = __builtin_amdgcn_s_memtime();      \
+  }
+#define FRA_WSTAMP_VAL(k, v)                                                                     \
+  if (lane == 0) {                                                                               \
+    const unsigned wi_ = blockIdx.x * gridDim.y + blockIdx.y;                                    \
+    if (wi_ < kWStampW) g_fra_wstamps[wi_ * kWStampN + (k)] = (unsigned long long)(v);            \
+  }
+// FRA_WSTAMP_FINE: the load phase split at forced waits (metadata, raw rows, LUT gathers + LDS stores)
+#ifdef FRA_WSTAMP_FINE
+#define FRA_WSTAMP_WAIT(k)                                      \
+  {                                                             \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    FRA_WSTAMP(k)                                               \
+  }
+#endif
+#endif
+#ifndef FRA_WSTAMP
+#define FRA_WSTAMP(k)
+#define FRA_WSTAMP_VAL(k, v)
+#endif
+#ifndef FRA_WSTAMP_WAIT
+#define FRA_WSTAMP_WAIT(k) {}
+#endif
+// phase-stop diagnostic builds (csrc/Makefile `wstops`, tools/pmc_stall_phases.sh): every subframe is first
+// described as VERBATIM (valid sizes: the frame scan and the assembly stay inside their buffers; the bytes
+// are meaningless), then the wave returns after phase k, keeping that phase's results alive through the
+// descriptor's unused cval
+#ifdef FRA_WSTOP
+#define FRA_WSTOP_AT(k, keep)                      \
+  if (FRA_WSTOP == (k)) {                          \
+    if (lane == 0) d->cval = (int32_t)(keep);      \
+    return;                                        \
+  }
+#define FRA_WSTOP_AT_T(k, keep)                    \
+  if (FRA_WSTOP == (k)) {                          \
+    if (lane == 0) d->cval = (int32_t)(keep);      \
+    return true;                                   \
+  }
+#else
+#define FRA_WSTOP_AT(k, keep)
+#define FRA_WSTOP_AT_T(k, keep)
+#endif
 
 // ---------------------------------------------------------------- frame header (RFC 9639 9.1)
 __host__ __device__ inline int utf8_len(uint32_t v) {

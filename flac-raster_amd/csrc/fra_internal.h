@@ -29,9 +29,17 @@ constexpr int kMaxModels = 5 + kMaxWin;  // fixed 0..4, one LPC order per apodiz
 // LDS sample array layout of k_analyze: each thread's 16-sample chunk at a stride of 20 words (4 pad
 // words), so the per-thread chunk reads (lane stride 20 dwords) are bank-conflict free for
 // ds_read_b32..b128; one zeroed chunk in front stands in for the samples before the block start.
+// The 32-bit array (32-bps analysis) pads 2 words per chunk instead (8-byte aligned chunks, 2-way conflicts):
+// 2 KiB less LDS, so the 32-bps workgroup fits 32 KiB (5 per CU).
 constexpr int kSmpStride = kChunk + 4;
 constexpr int kSmpWords = (kMaxBlock / kChunk + 1) * kSmpStride;
-FRA_HD int sidx(int i) { return kSmpStride + i + ((i >> 4) << 2); }
+template <typename T>
+FRA_HD constexpr int smp_stride() { return sizeof(T) == 4 ? kChunk + 2 : kChunk + 4; }
+template <typename T>
+FRA_HD constexpr int smp_words() { return (kMaxBlock / kChunk + 1) * smp_stride<T>(); }
+// sample i of the array smp (its element type picks the layout)
+template <typename T>
+FRA_HD int sidx(const T*, int i) { return smp_stride<T>() + i + (i >> 4) * (smp_stride<T>() - kChunk); }
 
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {
