@@ -39,7 +39,7 @@ int frame_scan_blocks(int nframes);
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
                              unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
                              unsigned tbase, unsigned tag, hipStream_t s);
-hipError_t launch_assemble(const JobArgs& a, hipStream_t s, int bg_blocks);
+hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
                                 hipStream_t s, unsigned long long* host_mirror = nullptr);
@@ -158,11 +158,9 @@ struct fra_plan {
   hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
   bool pack_pending[2] = {false, false};
   // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
-  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Whether a
-  // background workgroup co-resides with the analysis or takes an analysis workgroup's place depends on
-  // what the analysis leaves per SIMD: 16-bit plans (6 workgroups/CU) 32 VGPRs and 32 of 800 SGPRs (none
-  // fits), 32-bps plans (4/CU) 96 VGPRs, 288 SGPRs and 12.6 KiB of LDS per CU (k_minmax_vec and
-  // k_assemble_bg fit)
+  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Neither analysis
+  // leaves room beside it (k_analyze_w: 20 waves x 8 KiB fill the CU's LDS; 32-bps k_analyze: 5 workgroups of
+  // 31.6 KiB), so the background kernels run in the gaps between analysis waves
   NormDev* norm2[2] = {};
   int32_t* lut2[2] = {};
   hipStream_t nstream = nullptr;
@@ -769,11 +767,6 @@ static void use_buffers(fra_plan* p, int b) {
   p->args.norm = p->d_norm; p->args.lut = p->d_lut;
   p->cur = b;
 }
-// the pipelined execute's assembly kernel: k_assemble_bg (<= 32 VGPRs, one workgroup per CU) on 32-bps
-// plans, whose four analysis workgroups per CU leave room for it; k_assemble4 on 16-bit plans, where the
-// background form did not fit beside the analysis (SGPRs) and, made to fit, was slower than the per-frame
-// grid (r03 v7/v8)
-static bool pipe_asm_bg(const fra_plan* p) { return p->b32; }
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
   if (!p->pipe) return FRA_OK;
@@ -941,8 +934,6 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   // pipelined execute: the frame-size chain (k_frame_scan) only feeds this
   // execute's assembly, so it goes onto the pack stream with it and the plan's stream proceeds straight to
   // the next execute's analysis
-  // background form of k_assemble (<= 32 VGPRs, ~one workgroup per CU) beside the next execute's analysis
-  const int bg_blocks = (pack_st && pipe_asm_bg(p)) ? p->ncu : 0;
   if (pack_st && !ev_prev && !ev_pub && !host_mirror) {
     HIPCHK(hipEventRecord(ev_scan, st));
     HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
@@ -969,9 +960,9 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   if (pack_st) {  // assembly on the pack stream once this group's offsets exist
     HIPCHK(hipEventRecord(ev_scan, st));
     HIPCHK(hipStreamWaitEvent(pack_st, ev_scan, 0));
-    HIPCHK(launch_assemble(ga, pack_st, bg_blocks));
+    HIPCHK(launch_assemble(ga, pack_st));
   } else {
-    HIPCHK(launch_assemble(ga, st, bg_blocks));
+    HIPCHK(launch_assemble(ga, st));
   }
   return FRA_OK;
 }

@@ -1,5 +1,5 @@
-// fra_assemble.h -- frame assembly + CRC-16 of one frame by one wave (device code) for k_assemble4 and
-// k_assemble_bg (fra_pack.hip).
+// fra_assemble.h -- frame assembly + CRC-16 of one frame by one wave (device code) for k_assemble4
+// (fra_pack.hip).
 //
 // Emits what libFLAC's frame writer emits for every 4,096-sample block that
 // FLAC__stream_encoder_process_interleaved / _finish produce under the pyflac calls at
@@ -64,14 +64,6 @@ struct alignas(16) AssembleSmem {
   uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_scan); [wave]
   uint32_t tailw[4];    // the output window of the last, partial dword (bytes [4*NF - A, L)); [wave]
 };
-// background form: only the per-quad tables in LDS (9.3 KiB: it fits beside four 32-bps k_analyze
-// workgroups too); the once-per-frame tree levels 4..11 are read from global memory (L1/L2 resident)
-struct alignas(16) AssembleSmemBg {
-  uint16_t T[16][256];
-  uint16_t Mh[512];     // the Horner step x^(8*2^10)
-  uint32_t meta[4][kMetaWords];
-  uint32_t tailw[4];
-};
 
 // `take` (1..32) bits at bit b of a big-endian word array, right-aligned
 __device__ __forceinline__ uint32_t bits_at(const uint32_t* w, uint32_t b, int take) {
@@ -84,16 +76,12 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 }
 
 // CRC tables to LDS (16-byte loads) so no step of the CRC chain waits on a global gather
-template <typename SM>
-__device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
-  constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
+__device__ __forceinline__ void copy_tables(const JobArgs& a, AssembleSmem& S) {
   const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
-  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kBg ? 10 : kMLo) * 512);
+  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
   uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
-  uint4* dM;
-  if constexpr (kBg) dM = reinterpret_cast<uint4*>(&S.Mh[0]);
-  else dM = reinterpret_cast<uint4*>(&S.M[0][0]);
-  constexpr int NTV = 16 * 256 * 2 / 16, NMV = (kBg ? 1 : kMLevels) * 512 * 2 / 16;  // uint4 counts
+  uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
+  constexpr int NTV = 16 * 256 * 2 / 16, NMV = kMLevels * 512 * 2 / 16;  // uint4 counts
   for (int i = (int)threadIdx.x; i < NTV + NMV; i += kThreads) {
     if (i < NTV) dT[i] = srcT[i];
     else dM[i - NTV] = srcM[i - NTV];
@@ -103,23 +91,15 @@ __device__ __forceinline__ void copy_tables(const JobArgs& a, SM& S) {
 // one frame by one wave (four frames per workgroup, no workgroup barrier per frame, the CRC tables copied
 // to LDS once for the four by the caller), U quads per lane per round.  Header and blob bounds come
 // precomputed by k_frame_scan, so every metadata load is issued in the first round
-template <int U, typename SM>
-__device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, SM& S) {
+template <int U>
+__device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, AssembleSmem& S) {
   constexpr int NT = 64;  // lanes per frame
   const int lane = (int)threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int t = lane;
-  constexpr bool kBg = std::is_same<SM, AssembleSmemBg>::value;
   uint32_t* const meta = S.meta[wv];
   uint32_t& tailw = S.tailw[wv];
-  const uint16_t* M;     // tree levels kMLo..9
-  const uint16_t* Mh;    // the Horner level: x^(128 NT) = x^(8 * 2^10)
-  if constexpr (kBg) {  // (copy_tables<SM> put the Horner level in S.Mh)
-    M = a.crctab + 1024 + kMLo * 512;
-    Mh = &S.Mh[0];
-  } else {
-    M = &S.M[0][0];
-    Mh = &S.M[10 - kMLo][0];
-  }
+  const uint16_t* const M = &S.M[0][0];            // tree levels kMLo..9
+  const uint16_t* const Mh = &S.M[10 - kMLo][0];   // the Horner level: x^(128 NT) = x^(8 * 2^10)
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |

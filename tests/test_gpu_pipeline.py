@@ -199,7 +199,7 @@ def test_cross_execute_pipelining_buffers():
 ])
 def test_pipelined_assembly_equals_serial(kind, bands, H, W, tile, dtype, level, norm):
     """Pipelined executes run the frame-size chain and the assembly of execute k on the pack stream beside
-    execute k+1's analysis (k_assemble_bg on 32-bps plans, k_assemble on 16-bit ones).  The output of
+    execute k+1's analysis (k_frame_scan + k_assemble4).  The output of
     execute 2, written into an output buffer poisoned after execute 1 and read after a device-wide barrier,
     must be byte-identical to the serial (timing-mode) execute's; so must the plan's own download; and
     sampled tiles must equal the oracle's frames."""
