@@ -153,7 +153,7 @@ struct fra_plan {
   hipStream_t pack = nullptr;
   // the analysis of buffer set b runs on astream[b] (highest priority): execute k+1's k_analyze is queued
   // on the other stream than execute k's, so its first workgroups fill the CUs that execute k's tail
-  // leaves idle instead of waiting for that kernel to end (16-bit plans; FRA_DUAL_ANA=0/1 forces)
+  // leaves idle instead of waiting for that kernel to end
   hipStream_t astream[2] = {};
   hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
   bool pack_pending[2] = {false, false};
@@ -1223,9 +1223,9 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
                          hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&p->d_gbase_mirror, p->h_gbase, 0));
   }
-  // experiment knobs (defaults = measured best): FRA_H2D_AHEAD bands of H2D ahead of the oldest band whose
-  // D2H is not yet issued (0 = unlimited; 1 measured best on C4: 21.3 vs 22.2 ms)
-  static const int ahead = getenv("FRA_H2D_AHEAD") ? atoi(getenv("FRA_H2D_AHEAD")) : 1;
+  // H2D runs at most one band ahead of the oldest band whose D2H is not yet issued (unlimited measured
+  // slower on C4: 22.2 vs 21.3 ms)
+  constexpr int ahead = 1;
   // the copies must not overwrite the device raster while earlier work of this plan still reads it
   HIPCHK(hipEventRecord(p->hev_start, s));
   HIPCHK(hipStreamWaitEvent(p->h2d, p->hev_start, 0));
