@@ -114,8 +114,10 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
                                                     int rows, int nrb, int nitems) {
   using T = typename RawType<SRC>::T;
   using VT = VecT<T, V>;
-  // loads in flight per thread: 48 bytes (<= 32 VGPRs with offsets and keys), 8 loads of narrow vectors
-  constexpr int U = sizeof(VT) >= 16 ? 3 : (sizeof(VT) >= 8 ? 6 : 8);
+  // loads in flight per thread: 64 bytes, so that 256 * U vectors divide a band block of rows * nv ~ 2048
+  // vectors (the host's block shape): whole rounds only -- with 48 bytes a third of the last round re-read
+  // vector E-1 (C4: 3,072 slots for 2,048 vectors per band)
+  constexpr int U = sizeof(VT) >= 16 ? 4 : 8;
   __shared__ uint32_t smn[4], smx[4];
   const int wv = threadIdx.x >> 6;
   // items (stream, block of `rows` rows) = (item / nrb, item % nrb); a full grid has one item per
