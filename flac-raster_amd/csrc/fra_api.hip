@@ -897,9 +897,13 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     ma.norm += gr.w0 + c0;
     if (ma.lut) ma.lut += (int64_t)(gr.w0 + c0) * a.lut_stride;
     const int vec = (p->mm_vec && (uintptr_t)p->d_raster % p->mm_vec == 0) ? p->mm_vec : 0;  // pointer alignment
-    // background norm stage: one workgroup per CU striding over the row blocks (it shares the CUs with
-    // k_analyze instead of filling them)
-    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, nst_s, norm_st ? p->ncu : 0));
+    // the norm stage of a pipelined execute: the full grid, one workgroup per row block, as in serial plans --
+    // measured against one workgroup per CU striding over the blocks (FRA_MM_PER_CU=n: n per CU): C4 step
+    // 1.666 -> 1.626 ms, 8-way share 0.292 -> 0.274 ms, 4-way 0.505 -> 0.488 ms, C5 neutral, C3 1.089 -> 1.101
+    // (profiles/r04_ab_assemble_fpw_minmax_grid.txt, r04_ab_minmax_grid_shards.txt)
+    static const int mm_per_cu = getenv("FRA_MM_PER_CU") ? atoi(getenv("FRA_MM_PER_CU")) : 0;
+    HIPCHK(launch_minmax(p->src, ma, nc, p->max_segs, vec, p->mm_rows, p->mm_max_rows, nst_s,
+                         norm_st ? mm_per_cu * p->ncu : 0));
     HIPCHK(launch_norm_finalize(ma, nc, nst_s));
     HIPCHK(launch_norm_lut(p->src, ma, nc, nst_s));
   }
