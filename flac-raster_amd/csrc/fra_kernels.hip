@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
   __shared__ uint32_t smn[4], smx[4];
   const int wv = threadIdx.x >> 6;
   // items (stream, block of `rows` rows) = (item / nrb, item % nrb); a full grid has one item per
-  // workgroup, the background grid of the pipelined plan (one workgroup per CU) strides over them
+  // workgroup (the default, serial and pipelined); a smaller grid (FRA_MM_PER_CU) strides over them
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const int si = item / nrb;
     const StreamDev st = streams[si];
