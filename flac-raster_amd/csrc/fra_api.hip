@@ -739,10 +739,10 @@ static int plan_build(fra_plan* p) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(hipStreamCreateWithPriority(&p->pack, hipStreamNonBlocking, lo));
-        // 16-bit plans: C4 -1.2 %, C3 -2.4 %; 32-bps plans keep one analysis stream (C5 +5 %: the early
-        // start takes the slots the background assembly was using) (r03 v14)
-        if (!p->b32)
-          for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
+        // 16-bit plans: C4 -1.2 %, C3 -2.4 % (r03 v14); 32-bps plans too since the background assembly that the
+        // early start displaced is gone (r03: C5 +5 % with it; r04: C5 106.50 -> 106.24 ms,
+        // profiles/r04_ab_dual_streams_32bps.txt)
+        for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
       }
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
