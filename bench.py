@@ -266,6 +266,28 @@ def inrun_pmc(args, kernel):
     return res
 
 
+def codegen_stats(kernel):
+    """code bytes, VGPRs, SGPRs and spill counts of ``kernel`` in the loaded library's gfx950 code object
+    (tools/codeobj_stats.py), so codegen regressions show up in the bench record."""
+    try:
+        sys.path.insert(0, str(ROOT / "tools"))
+        import codeobj_stats
+        rows = [r for r in codeobj_stats.stats(str(N_LIB_PATH()), kernel) if r["kernel"].split("I")[0].endswith(kernel)
+                or f"{len(kernel)}{kernel}" in r["kernel"]]
+        if not rows:
+            return None
+        r = max(rows, key=lambda r: r["code_bytes"])
+        return {k: r.get(k) for k in ("kernel", "code_bytes", "vgpr", "sgpr", "sgpr_spill", "vgpr_spill", "lds",
+                                      "scratch", "s_nop", "writelane", "readlane")}
+    except Exception as e:  # reported, never fatal
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def N_LIB_PATH():
+    from flac_raster import _native
+    return _native._LIB_PATH
+
+
 def inrun_kernel_stats(args, out_dir):
     """rocprofv3 --kernel-trace --stats over a child run that executes ONLY the plan (``--child``: the
     warmup + timed executes of this config, no parity launches, no CPU / e2e legs) in the roofline's serial
@@ -519,8 +541,11 @@ def main():
         if not args.no_e2e and world == 1:
             if raster_bytes <= (8 << 30):
                 e2e = measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, plan)
-            else:
-                e2e = {"value": None, "note": "skipped by default above 8 GiB of raster (page-locked host copies)"}
+            else:  # the whole raster is never page-locked: the bounded ring path (fra_plan_encode_ring)
+                try:
+                    e2e = measure_e2e_ring(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, plan)
+                except Exception as e:  # reported, never fatal for the headline line
+                    e2e = {"value": None, "error": f"{type(e).__name__}: {e}"}
         # size vs libFLAC: only pinned for C2 (sample_rgb, 178,857 frame bytes at -c 5)
         size_c2 = None
         try:
@@ -552,6 +577,12 @@ def main():
                 pm = None
         if pm is None:
             pm = committed_profile(args, cfg, dom_name)
+        # the kernel the analysis phase's HIP events time: k_analyze_w (+ the partial-frame k_analyze list beside
+        # it) on 16-bit LUT plans at levels 3-6, k_analyze otherwise (inrun_pmc names the group)
+        dom_label = dom_name
+        if pm.get("kernels"):
+            dom_label = "k_analyze_w (+ k_analyze over the partial-frame list, same phase)"
+        codegen = codegen_stats("k_analyze_w" if pm.get("kernels") else dom_name)
         hbm_frac = achieved / HBM_PEAK_GBPS
         valu_frac = None
         if pm.get("valu_insts") and pm.get("busy_cycles_per_xcd"):
@@ -582,11 +613,17 @@ def main():
                        "serial_ms_per_step": round(step_ms_local, 4)},
             "per_rank": per_rank,
             "imbalance": round(T / mean_t, 4) if mean_t > 0 else None,
-            "roofline": {"bound": bound, "kernel": dom_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+            "roofline": {"bound": bound, "kernel": dom_label, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": pm.get("traffic"),
                          "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,
-                         "whole_path_frac": round(path_gbps / HBM_PEAK_GBPS, 5),
-                         "whole_path_gbps": round(path_gbps, 2),
+                         # whole path: algorithmic bytes of the step over the TIMED (pipelined) step, and over the
+                         # serial sum of the kernels (each alone, HIP events)
+                         "whole_path_frac": round(out_bytes_all / max(1e-12, T / args.steps) / 1e9 / HBM_PEAK_GBPS
+                                                  + raster_bytes * (world if weak else 1) / max(1e-12, T / args.steps)
+                                                  / 1e9 / HBM_PEAK_GBPS, 5),
+                         "whole_path_frac_serial": round(path_gbps / HBM_PEAK_GBPS, 5),
+                         "whole_path_gbps_serial": round(path_gbps, 2),
+                         "codegen": codegen,
                          "alg_bytes_per_launch": int(alg_bytes),
                          "kernel_ms_per_launch": {"minmax": round(per_launch_ms[0], 4),
                                                   "analyze": round(per_launch_ms[1], 4),
@@ -696,11 +733,74 @@ def measure_e2e(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, dev_plan):
     return res
 
 
+def measure_e2e_ring(N, ctx, cfg, dt, B, H, W, my_wins, my_px, dev_raster, dev_plan):
+    """Host raster -> frames in host memory with BOUNDED page-locked memory (``fra_plan_encode_ring``): the
+    scene sits in pageable host memory (copied there untimed, standing in for the source file's pages), a
+    producer copies its row bands into a page-locked ring of two host bands + a step (16 threads), and the
+    pipelined encoder copies each band H2D once the producer published it and releases its ring rows after
+    the copy; frames land in a lazily committed pageable buffer.  The PCIe floor is the raster's H2D at the
+    page-locked rate measured on the ring itself."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    host = np.empty((B, H, W), dt)  # pageable: the source
+    ctx.d2h(host, dev_raster)
+    nthreads = min(16, int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 4))
+    pool = ThreadPoolExecutor(nthreads)
+
+    def fill(dst, r0, r1):  # rows split over the threads (numpy copies release the GIL)
+        n = r1 - r0
+        k = max(1, min(nthreads, n))
+        cuts = [r0 + n * i // k for i in range(k + 1)]
+        list(pool.map(lambda i: np.copyto(dst[:, cuts[i] - r0:cuts[i + 1] - r0, :], host[:, cuts[i]:cuts[i + 1], :]),
+                      range(k)))
+
+    def run():
+        return N.encode_windows_ring((B, H, W), dt, my_wins, fill, cfg["level"], 4096, cfg["norm"],
+                                     device=ctx.device)
+
+    ref_i, ref_total = dev_plan.result()
+    dev_out, _ = dev_plan.device_output()
+    infos, frames, R = run()  # warm-up (pinned pool)
+    ref = np.empty(ref_total, np.uint8)
+    N.load().fra_memcpy_d2h(ctx.h, ref.ctypes.data, dev_out, ref_total)
+    equal = len(frames) == ref_total and bool(np.array_equal(frames, ref))
+    del ref, frames
+    t0 = time.perf_counter()
+    infos, frames, R = run()
+    te = time.perf_counter() - t0
+    total = len(frames)
+    del frames
+    # page-locked H2D rate on a ring-sized buffer -> the floor for the whole raster
+    ring = N.pinned_empty((B, R, W), dt)
+    ring[...] = host[:, :R, :]
+    t0 = time.perf_counter()
+    ctx.h2d(dev_raster, ring)
+    t_h2d = time.perf_counter() - t0
+    h2d_gbs = ring.nbytes / t_h2d / 1e9
+    t0 = time.perf_counter()
+    fill(ring, 0, R)
+    t_fill = time.perf_counter() - t0
+    fill_gbs = ring.nbytes / t_fill / 1e9
+    floor_ms = host.nbytes / (h2d_gbs * 1e9) * 1e3
+    res = {"value": round(my_px / te / 1e6, 2), "unit": "MPix/s", "ms": round(te * 1e3, 2),
+           "what": "pageable host raster -> producer copies into a page-locked ring of 2 host bands + a step "
+                   f"({nthreads} threads) -> pipelined row-band H2D / kernels / D2H -> lazily committed host frames "
+                   "(fra_plan_encode_ring, 1 GPU)",
+           "ring_rows": int(R), "ring_bytes": int(ring.nbytes), "raster_bytes": int(host.nbytes),
+           "frame_bytes": int(total), "bytes_equal_device_path": equal,
+           "h2d_pinned_gbs": round(h2d_gbs, 2), "producer_copy_gbs": round(fill_gbs, 2),
+           "pcie_floor_ms": round(floor_ms, 2), "ratio_vs_pcie_floor": round(te * 1e3 / floor_ms, 3)}
+    del ring, host
+    pool.shutdown()
+    return res
+
+
 def measure_e2e_file(N, cfg, host, dev_plan, pcie_floor_ms):
     """File -> container bytes in memory (cli.py:553-602): the scene written once as a
     tiled deflate and once as a tiled LZW GeoTIFF (tile 512, predictor 2, native writer), then
-    ``encode_geotiff_streaming`` -- the decode of row band b+1 on a producer thread overlapped with the
-    H2D / kernels / D2H of band b (fra_plan_encode_host_progress) -- plus the container assembly.
+    ``encode_geotiff_streaming`` -- the decode of row band b+1 on a producer thread into the bounded ring,
+    overlapped with the H2D / kernels / D2H of band b (fra_plan_encode_ring, r05) -- plus the container
+    assembly.
     Decode alone (the same threaded decoder into page-locked memory) is timed separately."""
     from flac_raster.geo import Affine
     from flac_raster.streaming import encode_geotiff_streaming, streaming_parts

@@ -7,7 +7,7 @@
 // analyze_subframe(), bit for bit the same bytes as k_analyze.
 //
 // Scope: full 4096-sample frames of a <= 16-bit integer raster whose normalisation goes through the
-// per-tile table (k_norm_lut), 8-byte sample vectors, levels 0-6 (lag <= 8, <= 3 apodization windows):
+// per-tile table (k_norm_lut), 8-byte sample vectors, levels 3-6 (lag <= 8, <= 3 apodization windows):
 // the C3/C4 workloads.  Everything else (partial last frames, raw int16 input, levels 7-8, 32-bps and
 // the mid-side virtual channels) stays on k_analyze; the launcher runs it over the plan's list of partial
 // subframes (known at plan creation), so this kernel finishes every subframe it starts.
@@ -229,39 +229,36 @@ __device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, i
 
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
 // lane l loads the 8-byte vectors l + 64k (all issued before the first use), gathers each sample's audio
-// value from the tile's table, packs int16 pairs and stores 4 samples per ds_write_b64
-template <int SRC>
+// value from the tile's table, packs int16 pairs and stores 4 samples per ds_write_b64.  Templated on the
+// element size only: the table index is the raw bit pattern (lut_index), the same for u8/i8 and u16/i16.
+// The row walk adds the uniform step = qs w + rs per vector (col < w, so at most one more wrap): no
+// division per vector for any width (a per-vector division was 14 KiB of this kernel's code)
+template <typename T>
 __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st, const FrameDev& fr, int c,
                                           const int32_t* lut, uint32_t* sw, int lane, uint32_t& orv, int32_t& vmin,
                                           int32_t& vmax, bool stamp) {
-  using T = typename RawType<SRC>::T;
   constexpr int V = 8 / (int)sizeof(T);
   constexpr int NV = kMaxBlock / 64 / V;
-  constexpr int step = 64 * V;
+  constexpr uint32_t step = 64 * V;
   using VT = VecT<T, V>;
-  const int w = st.width;
+  const uint32_t w = (uint32_t)st.width;
   const char* b0 = (const char*)((const T*)base + st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride);
   const uint32_t rsb = (uint32_t)st.row_stride * (uint32_t)sizeof(T);
-  int col = fr.col0 + lane * V;
+  const uint32_t qs = step / w, rs = step - qs * w, rstep = qs * rsb;  // uniform
+  uint32_t col = (uint32_t)fr.col0 + (uint32_t)lane * V;
   uint32_t roff = 0;
   if (col >= w) {
-    const int q = (int)((unsigned)col / (unsigned)w);
+    const uint32_t q = col / w;
     col -= q * w;
-    roff = (uint32_t)q * rsb;
+    roff = q * rsb;
   }
   VT x[NV];
 #pragma unroll
   for (int kv = 0; kv < NV; kv++) {
-    x[kv] = *(const VT*)(b0 + (roff + (uint32_t)col * (uint32_t)sizeof(T)));
-    col += step;
-    if (col >= w) {
-      if (w >= step) { col -= w; roff += rsb; }
-      else {
-        const int q = (int)((unsigned)col / (unsigned)w);
-        col -= q * w;
-        roff += (uint32_t)q * rsb;
-      }
-    }
+    x[kv] = *(const VT*)(b0 + (roff + col * (uint32_t)sizeof(T)));
+    col += rs;
+    roff += rstep;
+    if (col >= w) { col -= w; roff += rsb; }
   }
   if (stamp) FRA_WSTAMP_WAIT(11)
   uint32_t orp = 0;
@@ -270,7 +267,7 @@ __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st,
   for (int kv = 0; kv < NV; kv++) {
     int32_t g[V];
 #pragma unroll
-    for (int e = 0; e < V; e++) g[e] = lut[lut_index<SRC>(x[kv].v[e])];
+    for (int e = 0; e < V; e++) g[e] = lut[(uint32_t)x[kv].v[e]];
     const int i = (lane + 64 * kv) * V;
 #pragma unroll
     for (int h = 0; h < V / 4; h++) {
@@ -377,12 +374,8 @@ k_analyze_w(JobArgs a, int src) {
   const void* const raster = a.raster;
   const int32_t* const lut = a.lut + (int64_t)fr.stream * a.lut_stride;
   auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx, bool first) {
-    switch (src) {  // wave-uniform
-      case ST_U8: wload_lut<ST_U8>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      case ST_I8: wload_lut<ST_I8>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      case ST_U16: wload_lut<ST_U16>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-      default: wload_lut<ST_I16>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first); break;
-    }
+    if (src == ST_U8 || src == ST_I8) wload_lut<uint8_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first);  // uniform
+    else wload_lut<uint16_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first);
   };
   load_samples(orv, vmin, vmax, true);
   orv = wave_or32(orv);
@@ -459,13 +452,11 @@ k_analyze_w(JobArgs a, int src) {
   // ---- running winner (FRA-1 3.8: first minimal estimate in model order)
   uint32_t west = 0xFFFFFFFFu;
   int wm = 99, wtype = 2, wo = 0, wsh = 0, wps = 0;
-  int32_t wq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t wk = 0;
-  auto offer = [&](uint32_t est, int m, int type, int o, int sh, const int32_t* q, int ps, uint32_t kreg) {
+  // (an LPC winner's coefficients stay in mv: model m = 5 + window)
+  auto offer = [&](uint32_t est, int m, int type, int o, int sh, int ps, uint32_t kreg) {
     if (est < west || (est == west && m < wm)) {
       west = est; wm = m; wtype = type; wo = o; wsh = sh; wps = ps; wk = kreg;
-#pragma unroll
-      for (int jq = 0; jq < 8; jq++) wq[jq] = q ? q[jq] : 0;
     }
   };
 
@@ -497,17 +488,11 @@ k_analyze_w(JobArgs a, int src) {
   // ---- 3. LPC analysis per apodization window (3.4-3.7): lane 16 wi + o_l of window wi's lane group holds
   // that window's model (order o_l, quantised q, shift qsh, ok)
   int nlpc = 0;
-  // LPC model per window (levels 3-6: <= 3 windows): qlp coefficients, shift, order (0: none), usable
-  int32_t mq[kWinW][8], msh[kWinW], mo[kWinW];
-  bool mok[kWinW];
-#pragma unroll
-  for (int wi = 0; wi < kWinW; wi++) {
-    mo[wi] = 0;
-    mok[wi] = false;
-    msh[wi] = 0;
-#pragma unroll
-    for (int jx = 0; jx < 8; jx++) mq[wi][jx] = 0;
-  }
+  // LPC model per window (levels 3-6: <= 3 windows), lane-distributed in ONE VGPR instead of 33 scalars
+  // (scalar copies of every model spilled to VGPR lanes: 153 SGPR spill slots): lane 8 wi + jx = qlp
+  // coefficient jx of window wi, lane 24 + wi = its shift | usable order << 8 (0: none / not quantisable).
+  // Read back per candidate by v_readlane with a uniform lane index
+  uint32_t mv = 0;
   if constexpr (MAXLAG > 0) {
     if (cfg.nsub > 0 && lmax > 0) {
       nlpc = a.nwin;
@@ -634,31 +619,26 @@ k_analyze_w(JobArgs a, int src) {
       int qsh = 0;
       if (on) ok = quantize<MAXLAG>(lpo, lo, prec, q, qsh);
       const int o_l = nord > 0 ? (int)__builtin_ctz(rowbits | 0x10000u) : 0;
-      // each window's model (lane 16 wi + o) to scalar registers for the candidate loop (o = 0: none)
+      // each window's model (lane 16 wi + o_wi) gathered into mv (o = 0: none): lane l < 24 takes coefficient
+      // l & 7 of window l >> 3, lane 24 + wi the shift and usable order (every ds_bpermute on all 64 lanes)
+      const int dwi = lane < 24 ? lane >> 3 : (lane - 24) & 3;
+      const int ow = (int)bperm32((uint32_t)o_l, 16 * dwi);
+      const int L = 16 * dwi + ow;
+      const uint32_t info = (uint32_t)qsh | ((ow > 0 && ok) ? (uint32_t)lo << 8 : 0u);
+      const uint32_t vinfo = bperm32(info, L);
 #pragma unroll
-      for (int wi = 0; wi < kWinW; wi++) {
-        if (wi < nwin) {
-          const int ow = __builtin_amdgcn_readlane(o_l, 16 * wi);
-          const int L = 16 * wi + ow;
-          mo[wi] = ow;
-          mok[wi] = ow > 0 && __builtin_amdgcn_readlane((int)ok, L) != 0;
-          msh[wi] = __builtin_amdgcn_readlane(qsh, L);
-#pragma unroll
-          for (int jx = 0; jx < 8; jx++) mq[wi][jx] = __builtin_amdgcn_readlane(q[jx], L);
-        }
+      for (int jx = 0; jx < 8; jx++) {
+        const uint32_t vq = bperm32((uint32_t)q[jx], L);
+        mv = (lane & 7) == jx ? vq : mv;
       }
+      mv = lane >= 24 ? vinfo : mv;
+      mv = (lane < 24 ? dwi : lane - 24) < nwin && lane < 27 ? mv : 0u;
     }
   }
   FRA_WSTAMP(5)
 #ifdef FRA_WSTOP
   {
-    uint32_t kx = 0;
-#pragma unroll
-    for (int wi = 0; wi < kWinW; wi++) {
-      kx ^= (uint32_t)msh[wi] ^ ((uint32_t)mo[wi] << 8) ^ (mok[wi] ? 1u << 16 : 0u);
-#pragma unroll
-      for (int jx = 0; jx < 8; jx++) kx ^= (uint32_t)mq[wi][jx] << jx;
-    }
+    const uint32_t kx = wave_or32(mv ^ (uint32_t)lane);
     FRA_WSTOP_AT(5, kx)
   }
 #endif
@@ -668,10 +648,9 @@ k_analyze_w(JobArgs a, int src) {
   // The last window with a model is summed last: its pass replaces each chunk's samples in LDS by the
   // chunk's zig-zag residuals (int16 pairs), which the exact pass and the encoder then read instead of
   // recomputing the predictor twice (fallback: the samples are loaded again)
-  int keep_wi = -1;
-#pragma unroll
-  for (int wi = 0; wi < kWinW; wi++)
-    if (mok[wi]) keep_wi = wi;
+  // windows with a usable model (lanes 24 + wi of mv with an order)
+  const uint32_t okm = (uint32_t)(__ballot(lane >= 24 && lane < 24 + kWinW && (mv >> 8) != 0) >> 24);
+  const int keep_wi = okm ? 31 - __clz((int)okm) : -1;
   bool kept_fit = false;
   uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
 #pragma unroll 1
@@ -684,13 +663,14 @@ k_analyze_w(JobArgs a, int src) {
       psum = ci == 0 ? pf1 : pf2;
     } else {
       const int wi = ci - 2;
-      if (!(wi == 0 ? mok[0] : wi == 1 ? mok[1] : mok[2])) continue;  // no order / not quantisable
-      o = wi == 0 ? mo[0] : wi == 1 ? mo[1] : mo[2];
+      if (!((okm >> wi) & 1u)) continue;  // no order / not quantisable
+      const uint32_t inf = (uint32_t)__builtin_amdgcn_readlane((int)mv, 24 + wi);
+      o = (int)(inf >> 8);
       m = 5 + wi;
       type = 3;
-      sh = wi == 0 ? msh[0] : wi == 1 ? msh[1] : msh[2];
+      sh = (int)(inf & 0xFFu);
 #pragma unroll
-      for (int jx = 0; jx < 8; jx++) qm[jx] = wi == 0 ? mq[0][jx] : wi == 1 ? mq[1][jx] : mq[2][jx];
+      for (int jx = 0; jx < 8; jx++) qm[jx] = __builtin_amdgcn_readlane((int)mv, 8 * wi + jx);
       if (wi == keep_wi) {
         uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll 1
@@ -749,7 +729,7 @@ k_analyze_w(JobArgs a, int src) {
     uint32_t kreg;
     porder_search_reg(psum, P, pm, n, o, lane, best, bp, kreg);
     const uint64_t est = hdr + (uint64_t)o * sbps + (type == 3 ? 9 + (uint64_t)o * prec : 0) + best;
-    offer((uint32_t)est, m, type, o, sh, qm, bp, kreg);
+    offer((uint32_t)est, m, type, o, sh, bp, kreg);
   }
 
   FRA_WSTAMP(6)
@@ -763,6 +743,9 @@ k_analyze_w(JobArgs a, int src) {
   // A kept subframe that is not smaller than VERBATIM, or whose encode would overrun its residuals in the
   // aliased buffer, takes the second instance after the samples are loaded again: every full frame ends here
   const int type = wtype, o = wo, sh = wsh, ps = wps;
+  int32_t wq[8];
+#pragma unroll
+  for (int jq = 0; jq < 8; jq++) wq[jq] = type == 3 ? __builtin_amdgcn_readlane((int)mv, 8 * (wm - 5) + jq) : 0;
   const bool kept_w = type == 3 && wm == 5 + keep_wi && kept_fit;
   FRA_WSTAMP_VAL(9, kept_w ? 0 : (type != 3 ? 3 : (wm != 5 + keep_wi ? 4 : 5)))  // why the sample path
   auto reload = [&]() {  // the keep pass replaced the samples: load them once more
@@ -774,7 +757,6 @@ k_analyze_w(JobArgs a, int src) {
     if (w) shift_wasted();
     wsync();
   };
-  if (!kept_w && keep_wi >= 0) reload();
   const int pz = n >> ps;
   const int tl = 8 - ps;                  // log2 chunks per partition (2..8)
   const int ls = tl < 6 ? tl : 6;         // lanes per partition group inside one iteration
@@ -1065,8 +1047,10 @@ k_analyze_w(JobArgs a, int src) {
     return true;
   };
   // the kept instance hands a VERBATIM or overrunning subframe to the sample path (samples loaded again)
+  // the kept instance hands a VERBATIM or overrunning subframe to the sample path (samples loaded again; one
+  // call site of the reload)
   if (!kept_w || !tail(std::true_type{})) {
-    if (kept_w) reload();
+    if (keep_wi >= 0) reload();
     tail(std::false_type{});
   }
 }

@@ -37,8 +37,8 @@ hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, i
                                hipStream_t s);
 int frame_scan_blocks(int nframes);
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
-                             unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
-                             unsigned tbase, unsigned tag, hipStream_t s);
+                             unsigned long long* host_mirror, unsigned long long* look2, int look_stride,
+                             unsigned long long* ctl, hipStream_t s);
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s);
 hipError_t launch_group_offsets(unsigned long long* frame_off, const unsigned long long* frame_bytes,
                                 unsigned long long* gbase, int grp, int f0, int n, int last, int nframes,
@@ -114,9 +114,9 @@ struct fra_plan {
   // timing pass: slot 0) and, on the host, each slot's ticket base and launch tag (launches on one slot
   // are stream-ordered)
   unsigned long long* d_look = nullptr;
-  unsigned* d_ticket = nullptr;
+  uint32_t* d_err = nullptr;  // JobArgs::err (plan_sync_all)
+  unsigned long long* d_ticket = nullptr;  // per scan slot: [63:32] epoch, [31:0] next ticket (k_frame_scan)
   int look_stride = 0;
-  std::vector<unsigned> scan_tbase, scan_tag;
   uint16_t* d_crctab = nullptr;
   uint32_t* d_tmp = nullptr;
   uint32_t* d_fmeta = nullptr;
@@ -355,6 +355,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_out);
   (void)hipFree(p->d_look);
   (void)hipFree(p->d_ticket);
+  (void)hipFree(p->d_err);
   (void)hipFree(p->d_crctab);
   (void)hipFree(p->d_tmp);
   (void)hipFree(p->d_fmeta);
@@ -626,12 +627,13 @@ static int plan_build(fra_plan* p) {
     const int nslot = (int)p->groups.size();
     // any group of <= nfr frames needs <= 256 words by default, or nfr's count (one frame per thread when forced)
     p->look_stride = std::max({256, frame_scan_blocks(nfr), (nfr + 255) / 256});
-    HIPCHK(hipMalloc(&p->d_look, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
-    HIPCHK(hipMemset(p->d_look, 0, sizeof(unsigned long long) * (size_t)p->look_stride * nslot));
-    HIPCHK(hipMalloc(&p->d_ticket, sizeof(unsigned) * nslot));
-    HIPCHK(hipMemset(p->d_ticket, 0, sizeof(unsigned) * nslot));
-    p->scan_tbase.assign(nslot, 0u);
-    p->scan_tag.assign(nslot, 0u);
+    HIPCHK(hipMalloc(&p->d_look, sizeof(unsigned long long) * (size_t)p->look_stride * 2 * nslot));
+    HIPCHK(hipMemset(p->d_look, 0, sizeof(unsigned long long) * (size_t)p->look_stride * 2 * nslot));
+    HIPCHK(hipMalloc(&p->d_ticket, sizeof(unsigned long long) * nslot));
+    HIPCHK(hipMemset(p->d_ticket, 0, sizeof(unsigned long long) * nslot));
+    HIPCHK(hipMalloc(&p->d_err, sizeof(uint32_t)));
+    HIPCHK(hipMemset(p->d_err, 0, sizeof(uint32_t)));
+    p->args.err = p->d_err;
     HIPCHK(hipMalloc(&p->d_gbase, sizeof(unsigned long long) * (std::max(p->groups.size(), p->hbands.size()) + 1)));
     for (size_t g = 1; g < p->groups.size(); g++) {
       hipStream_t st = nullptr;
@@ -693,6 +695,7 @@ static int plan_build(fra_plan* p) {
   a.crctab = p->d_crctab;
   a.tmp = p->d_tmp;
   a.fmeta = p->d_fmeta;
+  a.err = p->d_err;
   a.out_cap = p->out_cap;
   a.tmp_stride = p->tmp_stride;
   a.lut = p->d_lut;
@@ -762,7 +765,7 @@ static void use_buffers(fra_plan* p, int b) {
   p->d_sf = p->sf2[b]; p->d_tmp = p->tmp2[b]; p->d_fmeta = p->fmeta2[b];
   p->d_fbytes = p->fbytes2[b]; p->d_foff = p->foff2[b];
   p->d_norm = p->norm2[b]; p->d_lut = p->lut2[b];
-  p->args.sf = p->d_sf; p->args.tmp = p->d_tmp; p->args.fmeta = p->d_fmeta;
+  p->args.sf = p->d_sf; p->args.tmp = p->d_tmp; p->args.fmeta = p->d_fmeta; p->args.err = p->d_err;
   p->args.frame_bytes = p->d_fbytes; p->args.frame_off = p->d_foff;
   p->args.norm = p->d_norm; p->args.lut = p->d_lut;
   p->cur = b;
@@ -795,6 +798,14 @@ static int plan_sync_all(fra_plan* p) {
   if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
   if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
   HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  // device-detected inconsistencies (JobArgs::err): bit 0 a frame-scan ticket past its grid, bit 1 a frame the
+  // assembly did not write because its sizes left the output or its slots -- the stream is not handed back
+  if (p->d_err) {
+    uint32_t e = 0;
+    HIPCHK(hipMemcpy(&e, p->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e) return set_err(FRA_E_STATE, "device error word 0x%x (%s%s)", e, (e & 1u) ? "frame-scan ticket desync " : "",
+                          (e & 2u) ? "frame outside its output/slot bounds" : "");
+  }
   return FRA_OK;
 }
 
@@ -914,6 +925,9 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   // the norm stream right after the norm stage (a whole execute before the frame scan that waits for them),
   // else beside k_analyze_w on the side stream
   const bool wave = wave_path(p);
+  // (tests: FRA_REQUIRE_WAVE=1 makes a plan that would not take the wave path fail instead)
+  static const bool require_wave = getenv("FRA_REQUIRE_WAVE") && atoi(getenv("FRA_REQUIRE_WAVE")) == 1;
+  if (require_wave && !wave && nf > 0) return set_err(FRA_E_STATE, "FRA_REQUIRE_WAVE: the plan does not take k_analyze_w");
   const auto plo = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f0 * 8);
   const auto phi = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f1 * 8);
   const int npart = wave ? (int)(phi - plo) : 0;
@@ -950,10 +964,8 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   // the previous group has published it
   if (nf > 0) {
     const int sl = slot < 0 ? gi : slot;
-    const unsigned tag = ++p->scan_tag[sl];
     HIPCHK(launch_frame_scan(ga, p->d_gbase, gi, gi == ng - 1, ev_prev ? 0 : 1, host_mirror,
-                             p->d_look + (size_t)sl * p->look_stride, p->d_ticket + sl, p->scan_tbase[sl], tag, st));
-    p->scan_tbase[sl] += (unsigned)frame_scan_blocks(nf);
+                             p->d_look + (size_t)sl * 2 * p->look_stride, p->look_stride, p->d_ticket + sl, st));
   }
   if (ev_prev) HIPCHK(hipStreamWaitEvent(st, ev_prev, 0));
   if (nf == 0 || ev_prev)
@@ -1172,8 +1184,37 @@ static int copy_rows_h2d(fra_plan* p, const uint8_t* host, int64_t r0, int64_t r
   return FRA_OK;
 }
 
+// the bounded-memory input of fra_plan_encode_ring: image row r of channel c at ring row r % rows
+struct RingIn {
+  const uint8_t* ring;
+  int64_t rows;
+  volatile int64_t* rows_done;
+};
+// H2D of raster rows [r0, r1) from the ring: per channel (run) at most two pieces, split where the ring wraps
+static int copy_rows_ring_h2d(fra_plan* p, const RingIn& rg, int64_t r0, int64_t r1, hipStream_t st) {
+  const fra_job& j = p->job;
+  const int es = elem_size(j.dtype);
+  const int64_t extent = (int64_t)(p->raster_bytes / es);
+  const bool planar = j.channels > 1 && j.band_stride >= j.row_stride;
+  const int nrun = planar ? j.channels : 1;
+  for (int c = 0; c < nrun; c++) {
+    const int64_t dbase = (int64_t)c * (planar ? j.band_stride : 0);
+    const int64_t hbase = (int64_t)c * (planar ? rg.rows * j.row_stride : 0);
+    for (int64_t r = r0; r < r1;) {
+      const int64_t rr = r % rg.rows, n = std::min(r1 - r, rg.rows - rr);
+      const int64_t a = dbase + r * j.row_stride;
+      const int64_t b = std::min(extent, dbase + (r + n) * j.row_stride);
+      if (b > a)
+        HIPCHK(hipMemcpyAsync((uint8_t*)p->d_raster_owned + a * es, rg.ring + (hbase + rr * j.row_stride) * es,
+                              (size_t)(b - a) * es, hipMemcpyHostToDevice, st));
+      r += n;
+    }
+  }
+  return FRA_OK;
+}
+
 static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
-                       uint64_t* total_bytes, const volatile int64_t* rows_ready);
+                       uint64_t* total_bytes, const volatile int64_t* rows_ready, const RingIn* ring = nullptr);
 int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
                          uint64_t* total_bytes) {
   return encode_host(p, host_raster, host_out, capacity, total_bytes, nullptr);
@@ -1183,20 +1224,42 @@ int fra_plan_encode_host_progress(fra_plan* p, const void* host_raster, uint8_t*
   if (!rows_ready) return set_err(FRA_E_INVALID, "null rows_ready");
   return encode_host(p, host_raster, host_out, capacity, total_bytes, rows_ready);
 }
-// wait (host) until the producer has published rows [0, r1) of the raster; false if it reported failure
-static bool wait_rows(const volatile int64_t* rows_ready, int64_t r1) {
+int fra_plan_host_band_rows(fra_plan* p, int64_t* max_rows) {
+  if (!p || !max_rows) return set_err(FRA_E_INVALID, "null argument");
+  int64_t m = 0;
+  for (const auto& hb : p->hbands) m = std::max(m, hb.r1 - hb.r0);
+  *max_rows = m;
+  return FRA_OK;
+}
+int fra_plan_encode_ring(fra_plan* p, const void* ring, int64_t ring_rows, uint8_t* host_out, uint64_t capacity,
+                         uint64_t* total_bytes, const volatile int64_t* rows_ready, volatile int64_t* rows_done) {
+  if (!p || !ring || !rows_ready || !rows_done) return set_err(FRA_E_INVALID, "null argument");
+  int64_t mx = 0;
+  fra_plan_host_band_rows(p, &mx);
+  if (ring_rows < mx || ring_rows < 1)
+    return set_err(FRA_E_INVALID, "ring of %lld rows < the tallest host band (%lld rows)", (long long)ring_rows,
+                   (long long)mx);
+  const RingIn rg{(const uint8_t*)ring, ring_rows, rows_done};
+  return encode_host(p, ring, host_out, capacity, total_bytes, rows_ready, &rg);
+}
+// wait (host) until the producer has published rows [0, r1) of the raster; false if it reported failure.
+// `poll` runs on every spin (the ring path publishes finished H2D copies there, which the producer may need
+// before it can publish r1)
+extern "C++" template <typename F>
+static bool wait_rows(const volatile int64_t* rows_ready, int64_t r1, F&& poll) {
   if (!rows_ready) return true;
   for (int spin = 0;; spin++) {
     const int64_t r = __atomic_load_n(const_cast<const int64_t*>(rows_ready), __ATOMIC_ACQUIRE);
     if (r < 0) return false;
     if (r >= r1) return true;
+    poll();
     if (spin < 64) continue;
     struct timespec ts = {0, spin < 1024 ? 2000 : 50000};
     nanosleep(&ts, nullptr);
   }
 }
 static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
-                       uint64_t* total_bytes, const volatile int64_t* rows_ready) {
+                       uint64_t* total_bytes, const volatile int64_t* rows_ready, const RingIn* ring) {
   if (!p || (!host_raster && p->raster_bytes) || (!host_out && capacity)) return set_err(FRA_E_INVALID, "null argument");
   (void)hipSetDevice(p->ctx->device);
   hipStream_t s = p->ctx->stream;
@@ -1235,14 +1298,25 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
   HIPCHK(hipStreamWaitEvent(p->h2d, p->hev_start, 0));
   HIPCHK(hipStreamWaitEvent(p->d2h, p->hev_start, 0));
   const uint8_t* host = (const uint8_t*)host_raster;
+  // ring path: bands whose H2D copy is enqueued / known complete; completed bands free their ring rows
+  int copies = 0, copied = 0;
+  auto publish = [&]() {
+    if (!ring) return;
+    int64_t done = -1;
+    while (copied < copies && hipEventQuery(p->hev[2 * copied]) == hipSuccess) done = p->hbands[copied++].r1;
+    if (done >= 0) __atomic_store_n(const_cast<int64_t*>(ring->rows_done), done, __ATOMIC_RELEASE);
+  };
   auto enqueue_copy = [&](int b) -> int {
     const auto& hb = p->hbands[b];
-    if (!wait_rows(rows_ready, hb.r1)) return set_err(FRA_E_STATE, "the raster producer failed (rows_ready < 0)");
+    if (!wait_rows(rows_ready, hb.r1, publish))
+      return set_err(FRA_E_STATE, "the raster producer failed (rows_ready < 0)");
     if (hb.r1 > hb.r0) {
-      const int rc = copy_rows_h2d(p, host, hb.r0, hb.r1, p->h2d);
+      const int rc = ring ? copy_rows_ring_h2d(p, *ring, hb.r0, hb.r1, p->h2d) : copy_rows_h2d(p, host, hb.r0, hb.r1, p->h2d);
       if (rc) return rc;
     }
     HIPCHK(hipEventRecord(p->hev[2 * b], p->h2d));
+    copies = b + 1;
+    publish();
     return FRA_OK;
   };
   uint64_t beg = 0;
@@ -1282,18 +1356,21 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
     // the band's end offset reaches h_gbase by a kernel store (k_group_offsets), not by a copy-engine
     // command that would queue behind the H2D copies
     rc = run_group(p, p->hbands[b].g, b, nb, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p->d_gbase_mirror);
-    if (rc) return rc;
+    if (rc) return drained(rc);
     HIPCHK(hipEventRecord(p->hev[2 * b + 1], s));
     // bands already assembled: their D2H can start now (pageable sources make the H2D enqueue blocking)
     while (issued <= b && hipEventQuery(p->hev[2 * issued + 1]) == hipSuccess)
-      if ((rc = enqueue_d2h(issued++))) return rc;
+      if ((rc = enqueue_d2h(issued++))) return drained(rc);
+    publish();
   }
   while (issued < nb) {
     HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
-    if ((rc = enqueue_d2h(issued++))) return rc;
+    if ((rc = enqueue_d2h(issued++))) return drained(rc);
   }
   HIPCHK(hipStreamSynchronize(p->d2h));
   HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipStreamSynchronize(p->h2d));
+  publish();
   p->executed = true;
   if (total_bytes) *total_bytes = beg;
   if (over)

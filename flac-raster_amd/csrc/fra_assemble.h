@@ -134,7 +134,10 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, As
 #pragma unroll
     for (int i = 0; i < kMaxChannels; i++)
       inb = inb && (i >= C || sg[i + 2] - sg[i + 1] <= 32u * (uint32_t)a.tmp_stride);
-    if (!inb) return;
+    if (!inb) {
+      if (t == 0 && a.err) atomicOr(a.err, 2u);
+      return;
+    }
   }
 #ifdef FRA_GUARD
   const uint64_t TOT = a.out_cap;  // frame_off[nframes_total] is final only after the last frame group

@@ -219,6 +219,8 @@ struct JobArgs {
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
   const int32_t* part;     // k_analyze list mode (beside k_analyze_w): (frame * 8 + channel) of the partial
   int32_t npart;           //   subframes of the launch's frames, npart entries (null: the normal grid)
+  uint32_t* err;           // plan error word (checked at every sync): bit 0 frame-scan ticket desync, bit 1 a
+                           //   frame outside its output / slot bounds (not written)
 };
 
 }  // namespace fra

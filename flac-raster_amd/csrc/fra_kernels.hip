@@ -228,24 +228,46 @@ __device__ uint64_t frame_bytes_one(const JobArgs& a, int g) {
 // workgroups in TICKET order -- a workgroup only ever waits on workgroups that took an earlier ticket, so
 // are already running: no assumption on dispatch order or co-residency.  The look-back reads 64
 // predecessors per round (one per lane) and stops at the nearest inclusive prefix.  Look-back words:
-// [63:42] launch tag, [41:40] flag (1 aggregate, 2 inclusive prefix), [39:0] bytes (< 1 TiB per group);
-// the tag makes clearing them unnecessary; each word carries its own payload, so relaxed device-scope atomics
-// suffice (no acquire/release cache maintenance per look-back round).  add_base: the group's base offset gbase[grp] is ordered before
-// this launch -> final offsets, gbase[grp+1] (+ frame_off[nframes] for the last group, + the host mirror);
-// else group-relative offsets (k_group_offsets adds the base once the previous group is done).
-constexpr uint64_t kScanValMask = (1ull << 40) - 1;
+// [63:62] flag (0 not yet published, 1 aggregate, 2 inclusive prefix), [61:0] bytes; each word carries its
+// own payload, so relaxed device-scope atomics suffice (no acquire/release cache maintenance per look-back
+// round).  add_base: the group's base offset gbase[grp] is ordered before this launch -> final offsets,
+// gbase[grp+1] (+ frame_off[nframes] for the last group, + the host mirror); else group-relative offsets
+// (k_group_offsets adds the base once the previous group is done).
+//
+// The scan state lives on the device, so a launch needs no host-side counter (graph replays and failed
+// enqueues cannot desynchronise it): per slot one 64-bit control word, [63:32] epoch, [31:0] next ticket.
+// The workgroup that takes the launch's last ticket resets the ticket and advances the epoch (every other
+// ticket of the launch is already taken); launch epoch e publishes into half e & 1 of the slot's look-back
+// words and zeroes the other half for the next launch (launches on one slot are stream ordered).  A ticket
+// past the grid (a desynchronised control word) sets bit 0 of the plan's error word and publishes nothing.
+constexpr uint64_t kScanValMask = (1ull << 62) - 1;
+constexpr uint64_t kScanAgg = 1ull << 62, kScanInc = 2ull << 62;
 template <int ITEMS>  // frames per thread (contiguous): 256 * ITEMS per workgroup
 __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long long* gbase, int grp, int last,
                                                     int add_base, unsigned long long* host_mirror,
-                                                    unsigned long long* look, unsigned* ticket, unsigned tbase,
-                                                    unsigned tag) {
-  __shared__ unsigned s_t;
+                                                    unsigned long long* look2, int look_stride,
+                                                    unsigned long long* ctl) {
+  __shared__ unsigned s_t, s_half;
   __shared__ uint64_t s_w[4];
   __shared__ uint64_t s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) s_t = atomicAdd(ticket, 1u) - tbase;
+  if (tid == 0) {
+    const unsigned long long old = atomicAdd(ctl, 1ull);
+    const unsigned tk = (unsigned)old, ep = (unsigned)(old >> 32);
+    if (tk == gridDim.x - 1)
+      __hip_atomic_store(ctl, (unsigned long long)(ep + 1u) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk >= gridDim.x && a.err) atomicOr(a.err, 1u);
+    s_t = tk;
+    s_half = ep & 1u;
+  }
   __syncthreads();
+  if (s_t >= gridDim.x) return;  // (nobody waits on a ticket past the grid)
   const int t = (int)s_t;  // this workgroup's position in the scan
+  unsigned long long* const look = look2 + (size_t)s_half * look_stride;
+  {
+    unsigned long long* const nxt = look2 + (size_t)(s_half ^ 1u) * look_stride;
+    for (int i = t * 256 + tid; i < look_stride; i += (int)gridDim.x * 256) nxt[i] = 0ull;
+  }
   const int n = a.frame_count;
   const int i0 = (t * 256 + tid) * ITEMS;
   uint64_t fb[ITEMS], loc = 0;
@@ -270,17 +292,15 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
     agg += s_w[k];
   }
   if (wv == 0) {
-    const uint64_t tg = (uint64_t)(tag & 0x3FFFFFu) << 42;
     if (lane == 0)
-      __hip_atomic_store(&look[t], tg | ((t == 0 ? 2ull : 1ull) << 40) | (agg & kScanValMask), __ATOMIC_RELAXED,
+      __hip_atomic_store(&look[t], (t == 0 ? kScanInc : kScanAgg) | (agg & kScanValMask), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     for (int j0 = t - 1; j0 >= 0;) {
       // lane l looks at workgroup j0 - l; before workgroup 0: an inclusive prefix of 0
       const int j = j0 - lane;
-      const uint64_t w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : (tg | (2ull << 40));
-      const uint32_t fl = (w & ~((1ull << 42) - 1)) == tg ? (uint32_t)(w >> 40) & 3u : 0u;
+      const uint64_t w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kScanInc;
+      const uint32_t fl = (uint32_t)(w >> 62);
       const uint64_t incm = __ballot(fl == 2), nrdy = __ballot(fl == 0);
       const int stop = incm ? (int)__builtin_ctzll(incm) : 64;  // the nearest inclusive prefix
       const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
@@ -297,7 +317,7 @@ __global__ void __launch_bounds__(256) k_frame_scan(JobArgs a, unsigned long lon
     }
     if (lane == 0) {
       if (t > 0)
-        __hip_atomic_store(&look[t], tg | (2ull << 40) | ((excl + agg) & kScanValMask), __ATOMIC_RELAXED,
+        __hip_atomic_store(&look[t], kScanInc | ((excl + agg) & kScanValMask), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       s_excl = excl;
     }
@@ -416,13 +436,14 @@ int frame_scan_blocks(int nframes) {
   return (nframes + per - 1) / per;
 }
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
-                             unsigned long long* host_mirror, unsigned long long* look, unsigned* ticket,
-                             unsigned tbase, unsigned tag, hipStream_t s) {
+                             unsigned long long* host_mirror, unsigned long long* look2, int look_stride,
+                             unsigned long long* ctl, hipStream_t s) {
   if (a.frame_count > 0) {
     const int it = scan_items(a.frame_count), nb = frame_scan_blocks(a.frame_count);
-    if (it == 1) k_frame_scan<1><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
-    else if (it == 4) k_frame_scan<4><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
-    else k_frame_scan<16><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look, ticket, tbase, tag);
+    if (nb > look_stride) return hipErrorInvalidValue;
+    if (it == 1) k_frame_scan<1><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look2, look_stride, ctl);
+    else if (it == 4) k_frame_scan<4><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look2, look_stride, ctl);
+    else k_frame_scan<16><<<nb, 256, 0, s>>>(a, gbase, grp, last, add_base, host_mirror, look2, look_stride, ctl);
   }
   return hipGetLastError();
 }

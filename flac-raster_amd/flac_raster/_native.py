@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import time
 from pathlib import Path
 from typing import List, Optional, Sequence, Tuple
 
@@ -92,6 +93,7 @@ EXPORTS = [
     "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
     "fra_host_register", "fra_host_unregister", "fra_tiff_decode", "fra_plan_set_first_frame",
     "fra_plan_flags", "fra_plan_encode_host_progress", "fra_tiff_compress_bound", "fra_tiff_compress",
+    "fra_plan_encode_ring", "fra_plan_host_band_rows",
 ]
 
 
@@ -148,6 +150,8 @@ def load():
         L.fra_host_unregister.argtypes = [vp]
         L.fra_tiff_decode.argtypes = [vp, u64, C.POINTER(TiffLayout), C.POINTER(TiffChunk), i32, vp, i32]
         L.fra_plan_encode_host_progress.argtypes = [vp, vp, vp, u64, C.POINTER(u64), vp]
+        L.fra_plan_encode_ring.argtypes = [vp, vp, C.c_int64, vp, u64, C.POINTER(u64), vp, vp]
+        L.fra_plan_host_band_rows.argtypes = [vp, C.POINTER(C.c_int64)]
         L.fra_tiff_compress_bound.argtypes = [i32, u64]
         L.fra_tiff_compress_bound.restype = u64
         L.fra_tiff_compress.argtypes = [i32, i32, vp, u64, i32, vp, u64, C.POINTER(u64), i32]
@@ -412,6 +416,29 @@ class Plan:
         _check(rc)
         return total.value
 
+    def host_band_rows(self) -> int:
+        """Rows of the tallest host row band (``fra_plan_host_band_rows``)."""
+        m = C.c_int64()
+        _check(load().fra_plan_host_band_rows(self.h, C.byref(m)))
+        return m.value
+
+    def encode_ring(self, ring: np.ndarray, out: np.ndarray, rows_ready: np.ndarray, rows_done: np.ndarray) -> int:
+        """:meth:`encode_host_progress` with bounded host memory (``fra_plan_encode_ring``): ``ring`` is
+        ``(B, ring_rows, W)`` and holds image row r at ring row ``r % ring_rows``; the call publishes in
+        ``rows_done[0]`` the rows whose H2D copy completed (the producer may then reuse their ring rows)."""
+        for a in (rows_ready, rows_done):
+            if a.dtype != np.int64 or a.size < 1:
+                raise ValueError("rows_ready / rows_done must be int64 arrays of >= 1 element")
+        total = C.c_uint64()
+        self._keep = ring
+        rc = load().fra_plan_encode_ring(self.h, C.c_void_p(ring.ctypes.data), ring.shape[1],
+                                         C.c_void_p(out.ctypes.data), out.nbytes, C.byref(total),
+                                         C.c_void_p(rows_ready.ctypes.data), C.c_void_p(rows_done.ctypes.data))
+        if rc == E_SPACE:
+            raise OutputTooSmall(total.value)
+        _check(rc)
+        return total.value
+
     def frame_offsets(self, nframes: int) -> np.ndarray:
         """Byte offset of every frame in the concatenated output (+ total at the end)."""
         off = np.empty(nframes + 1, dtype=np.uint64)
@@ -522,6 +549,86 @@ def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize
         total = plan.encode_host(a, out) if rows_ready is None else plan.encode_host_progress(a, out, rows_ready)
         infos, _ = plan.result()
         return infos, out[:total]
+    finally:
+        plan.close()
+
+
+def ring_rows_for(band_rows: int, step: int, height: int) -> int:
+    """Ring height for :func:`encode_windows_ring`: two host bands + one producer step (so the producer
+    decodes band b+1 while band b is copied; band + step is the minimum that cannot deadlock), in whole
+    producer steps, capped at the raster height."""
+    step = max(1, step)
+    rows = -(-(2 * band_rows + step) // step) * step
+    return int(min(height, rows))
+
+
+def encode_windows_ring(shape, dtype, windows, fill, level: int = 5, blocksize: int = 4096, norm: int = 16,
+                        sample_rate: int = 0, device: int = 0, step: int = 0, ring_rows: int = 0):
+    """Encode windows of a band-planar raster of ``shape`` ``(B, H, W)`` that never exists whole in host
+    memory (``fra_plan_encode_ring``): a producer thread calls ``fill(dst, r0, r1)`` to write image rows
+    ``[r0, r1)`` of every band into ``dst`` (a ``(B, r1 - r0, W)`` view of a page-locked ring), in steps of
+    ``step`` rows (default: the tallest host band), top to bottom; each step waits until the encoder's H2D
+    copies have released its ring rows.  Host memory: the ring (``ring_rows`` rows, default
+    :func:`ring_rows_for`) + the frames (a lazily committed buffer: only the written bytes are resident).
+
+    Returns ``(infos, frames, ring_rows)`` as :func:`encode_windows_buffer` (``frames`` not page-locked)."""
+    B, H, W = shape
+    dt = np.dtype(dtype)
+    if dt not in DTYPE_CODES:
+        raise TypeError(f"unsupported dtype {dt}")
+    ctx = default_context(device)
+    plan = Plan(ctx, None, False, dt, B, (H * W, W, 1), windows, level, blocksize, norm, sample_rate)
+    th = None
+    rows_ready = np.zeros(1, np.int64)
+    rows_done = np.zeros(1, np.int64)
+    stop = []
+    try:
+        band = max(1, plan.host_band_rows())
+        step = int(step) if step and step > 0 else band
+        R = int(ring_rows) if ring_rows else ring_rows_for(band, step, H)
+        if R < min(H, band + step):
+            raise ValueError(f"ring of {R} rows < band {band} + step {step}")
+        ring = pinned_empty((B, R, W), dt)
+        cap, _ = plan.capacity()
+        out = np.empty(cap, np.uint8)  # pages are committed as the frames land
+        errors: list = []
+
+        def produce():
+            try:
+                r0 = 0
+                while r0 < H:
+                    r1 = min(H, r0 + step)
+                    while rows_done[0] < r1 - R:  # the encoder still copies these ring rows
+                        if stop:
+                            return
+                        time.sleep(0.0002)
+                    r = r0
+                    while r < r1:  # split where the ring wraps
+                        rr = r % R
+                        n = min(r1 - r, R - rr)
+                        fill(ring[:, rr:rr + n, :], r, r + n)
+                        r += n
+                    rows_ready[0] = r1
+                    r0 = r1
+            except BaseException as e:  # reported to the encoder (rows_ready = -1), re-raised below
+                errors.append(e)
+                rows_ready[0] = -1
+
+        th = threading.Thread(target=produce, name="ring-producer", daemon=True)
+        th.start()
+        try:
+            total = plan.encode_ring(ring, out, rows_ready, rows_done)
+        except BaseException:
+            stop.append(1)
+            th.join()
+            if errors:
+                raise errors[0]
+            raise
+        th.join()
+        if errors:
+            raise errors[0]
+        infos, _ = plan.result()
+        return infos, out[:total], R
     finally:
         plan.close()
 

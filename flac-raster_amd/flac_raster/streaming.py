@@ -25,7 +25,7 @@ from . import flac_meta
 from .converter import raster_metadata, raster_tags
 from .geo import Affine, window_transform
 from .tiff import GeoTIFF
-from .tiles import TileStream, calculate_tiles, encode_tiles
+from .tiles import TileStream, calculate_tiles, encode_tiles, encode_tiles_ring
 
 
 def tile_flac_parts(ts: TileStream, transform: Affine, crs: Optional[str], row_off: int, col_off: int, height: int,
@@ -96,8 +96,7 @@ def decode_while_encoding(g: GeoTIFF, tile_size: int):
     info = g.info
     raster = _alloc((info.count, info.height, info.width), info.dtype, True)
     rows_ready = np.zeros(1, np.int64)
-    step = max(tile_size, g.ch)
-    step = ((step + g.ch - 1) // g.ch) * g.ch if g.ch < info.height else info.height
+    step = decode_step(g, tile_size)
     errors: list = []
 
     def run():
@@ -116,10 +115,42 @@ def decode_while_encoding(g: GeoTIFF, tile_size: int):
     return raster, rows_ready, th
 
 
+def decode_step(g: GeoTIFF, tile_size: int) -> int:
+    """Rows per producer step: one tile row, rounded up to whole TIFF strips / tiles."""
+    info = g.info
+    step = max(tile_size, g.ch)
+    return ((step + g.ch - 1) // g.ch) * g.ch if g.ch < info.height else info.height
+
+
+def encode_geotiff_ring(g: GeoTIFF, tiles, compression_level: int = 5, device: int = 0, tile_size: int = 512,
+                        ring_rows: int = 0):
+    """GeoTIFF -> tile streams with bounded host memory: the file's row bands are decoded into a
+    page-locked ring (``tiles.encode_tiles_ring``) that the pipelined encoder copies from and recycles, so
+    the raster is never held whole -- as the reference, which reads one tile window at a time
+    (``cli.py:553-559``).  Returns ``(streams, ring_rows)``."""
+    info = g.info
+
+    def fill(dst, r0, r1):
+        g.read_window_into(dst, r0, 0, r1 - r0, info.width)
+
+    return encode_tiles_ring((info.count, info.height, info.width), info.dtype, tiles, fill, compression_level,
+                             device, step=decode_step(g, tile_size), ring_rows=ring_rows)
+
+
 def encode_geotiff_streaming(input_path: Path, tile_size: int = 512, compression_level: int = 5,
-                             devices: Optional[Sequence[int]] = None):
-    """GeoTIFF file -> (tiles, streams, raster info): decode and encode overlapped (decode_while_encoding)."""
+                             devices: Optional[Sequence[int]] = None, ring: bool = True):
+    """GeoTIFF file -> (tiles, streams, raster info): decode and encode overlapped.  One device: through
+    the bounded ring (``encode_geotiff_ring``); several: the whole raster is decoded into page-locked
+    memory (``decode_while_encoding``) and split over the devices."""
     g = GeoTIFF(input_path)
+    if ring and (not devices or len(devices) == 1):
+        try:
+            info = g.info
+            tiles = calculate_tiles(info.height, info.width, tile_size)
+            streams, _ = encode_geotiff_ring(g, tiles, compression_level, devices[0] if devices else 0, tile_size)
+            return tiles, streams, (info.count, info.height, info.width), np.dtype(info.dtype), info
+        finally:
+            g.close()
     raster, rows_ready, th = decode_while_encoding(g, tile_size)
     try:
         tiles = calculate_tiles(raster.shape[1], raster.shape[2], tile_size)

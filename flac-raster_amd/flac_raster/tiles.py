@@ -107,15 +107,34 @@ def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]]
             raise ValueError("rows_ready needs the group to start at raster row 0")
         infos, frames = _native.encode_windows_buffer(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
                                                       device=device, rows_ready=rows_ready)
-        res = []
-        mv = memoryview(frames)
-        for inf in infos:
-            hdr = _native.stream_header(inf.channels, inf.bps, inf.sample_rate, BLOCKSIZE)
-            res.append(TileStream(hdr, mv[inf.offset:inf.offset + inf.frame_bytes], float(inf.data_min),
-                                  float(inf.data_max), inf.sample_rate, inf.bps, inf.channels, inf.nframes))
-        out[slot] = res
+        out[slot] = streams_from(infos, frames)
     except BaseException as e:  # re-raised on the calling thread
         errors.append(e)
+
+
+def streams_from(infos, frames) -> List[TileStream]:
+    """TileStreams over one plan's output: zero-copy views of ``frames`` at each window's offset."""
+    res = []
+    mv = memoryview(frames)
+    for inf in infos:
+        hdr = _native.stream_header(inf.channels, inf.bps, inf.sample_rate, BLOCKSIZE)
+        res.append(TileStream(hdr, mv[inf.offset:inf.offset + inf.frame_bytes], float(inf.data_min),
+                              float(inf.data_max), inf.sample_rate, inf.bps, inf.channels, inf.nframes))
+    return res
+
+
+def encode_tiles_ring(shape, dtype, tiles: Sequence[Tuple[int, int, int, int]], fill, level: int = 5,
+                      device: int = 0, step: int = 0, ring_rows: int = 0) -> Tuple[List[TileStream], int]:
+    """:func:`encode_tiles` for a raster that is produced row band by row band and never held whole
+    (``_native.encode_windows_ring``): ``fill(dst, r0, r1)`` writes image rows ``[r0, r1)`` of every band
+    into ``dst``.  The reference reads each tile's window the same way (``cli.py:553-559``).  Returns the
+    streams and the ring's height in rows."""
+    if not tiles:
+        return [], 0
+    infos, frames, R = _native.encode_windows_ring(shape, dtype, tiles, fill, level=level, blocksize=BLOCKSIZE,
+                                                   norm=norm_bits(dtype), device=device, step=step,
+                                                   ring_rows=ring_rows)
+    return streams_from(infos, frames), R
 
 
 def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,

@@ -144,6 +144,19 @@ FRA_API int fra_plan_encode_host(fra_plan *plan, const void *host_raster, uint8_
  * either every row or -1 (also when it fails or is cancelled); the call waits without a time limit. */
 FRA_API int fra_plan_encode_host_progress(fra_plan *plan, const void *host_raster, uint8_t *host_out, uint64_t capacity,
                                           uint64_t *total_bytes, const volatile int64_t *rows_ready);
+/* The same pass with BOUNDED host memory for the raster (r05): the producer decodes into a ring of
+ * ring_rows rows per channel instead of the whole raster -- image row r of channel c lives at ring row
+ * r % ring_rows, the ring laid out (channels, ring_rows, row_stride) in the job's dtype (row_stride and
+ * col_stride as in the job; channel c at c * ring_rows * row_stride elements; pixel-interleaved jobs use
+ * one run).  *rows_ready as above; the call publishes in *rows_done (release store) the rows whose H2D copy
+ * has completed: the producer may write image row r once r < *rows_done + ring_rows.  ring_rows must hold
+ * the tallest host band (fra_plan_host_band_rows) plus the producer's own step, else FRA_E_INVALID.
+ * Replaces the reference's per-tile window read (cli.py:553-559), which also never holds the raster. */
+FRA_API int fra_plan_encode_ring(fra_plan *plan, const void *ring, int64_t ring_rows, uint8_t *host_out,
+                                 uint64_t capacity, uint64_t *total_bytes, const volatile int64_t *rows_ready,
+                                 volatile int64_t *rows_done);
+/* rows of the tallest host band of a plan (the ring of fra_plan_encode_ring must hold it) */
+FRA_API int fra_plan_host_band_rows(fra_plan *plan, int64_t *max_rows);
 /* frame number of every stream's first frame for the next execute (the job's first_frame until set) */
 FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */

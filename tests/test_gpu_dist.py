@@ -1,0 +1,57 @@
+"""The distributed product path on the GPU: two fresh child processes
+(started before either touches the GPU), both on device 0 with the gloo backend, each run
+``dist.encode_tiles_distributed`` with the real ``tiles.encode_tiles`` on their LPT share of a GeoTIFF (each
+decodes only its own windows), gathered through the node-local spool file -- the path one rank per GPU takes
+on an 8-GPU node (reference loop being sharded: cli.py:553-630).  The container must equal the
+single-process one byte for byte."""
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from flac_raster.streaming import create_streaming_flac
+from flac_raster.synth import synth_window
+from flac_raster.tiff import write_geotiff
+
+pytestmark = pytest.mark.gpu
+HERE = Path(__file__).resolve().parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,dtype,level,tile", [(2, np.uint16, 5, 512), (3, np.float32, 8, 256)])
+def test_distributed_gpu_container_equals_single_process(tmp_path, world, dtype, level, tile):
+    kind = 4 if dtype == np.uint16 else 5
+    r = synth_window(kind, 31, 3, 1800, 1500).astype(dtype)
+    src = tmp_path / "scene.tif"
+    write_geotiff(src, r, compression="deflate", tile=256, predictor=2 if dtype == np.uint16 else 3,
+                  transform=(10.0, 0.0, 300000.0, 0.0, -10.0, 5000040.0), crs="EPSG:32633")
+    out = tmp_path / "dist.flac"
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, str(HERE / "dist_gpu_worker.py"), str(k), str(world), str(port),
+                               str(src), str(tile), str(level), str(out)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for k in range(world)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    counts = [int(Path(f"{out}.rank{k}").read_text()) for k in range(world)]
+    assert all(c > 0 for c in counts)  # every rank encoded a share
+    single = tmp_path / "single.flac"
+    create_streaming_flac(src, single, tile, level)
+    assert out.read_bytes() == single.read_bytes()

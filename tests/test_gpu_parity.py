@@ -248,16 +248,32 @@ def test_two_channel_pyflac_path_mid_side():
     assert frames == O.encode(a32, 44100, level=5, with_header=False)
 
 
-# ---- k_analyze_w (one subframe per wave: full frames of <= 16-bit rasters, levels 0-6)
-@pytest.mark.parametrize("level", [0, 1, 3, 4, 5, 6])
+# ---- k_analyze_w (one subframe per wave: full frames of <= 16-bit LUT rasters, levels 3-6, 8-byte sample vectors)
+@pytest.fixture
+def require_wave(monkeypatch):
+    """The plan must take k_analyze_w (FRA_REQUIRE_WAVE=1: the library fails a plan that would not)."""
+    monkeypatch.setenv("FRA_REQUIRE_WAVE", "1")
+
+
+@pytest.mark.parametrize("level", [3, 4, 5, 6])
 @pytest.mark.parametrize("dtype", ["uint8", "int16"])
-def test_wave_kernel_levels_dtypes(level, dtype):
+def test_wave_kernel_levels_dtypes(require_wave, level, dtype):
     """Every level the wave kernel takes, both LUT widths, full + partial frames (partial ones go to
-    k_analyze through the frame list) against the oracle."""
-    r = synth_window(4 if dtype == "uint8" else 3, 7 + level, 2, 300, 700).astype(np.float64)
+    k_analyze through the frame list) against the oracle.  Window columns and widths keep every 8-byte
+    sample vector inside a row (the wave path's condition), which FRA_REQUIRE_WAVE checks."""
+    r = synth_window(4 if dtype == "uint8" else 3, 7 + level, 2, 300, 704).astype(np.float64)
     info = np.iinfo(dtype)
     r = np.clip(r / r.max() * (info.max - info.min) + info.min, info.min, info.max).astype(dtype)
-    check_windows(r, [(0, 0, 300, 700), (0, 0, 64, 64), (17, 9, 131, 257)], level, 16)
+    check_windows(r, [(0, 0, 300, 704), (0, 0, 64, 64), (17, 8, 131, 256)], level, 16)
+
+
+def test_require_wave_rejects_other_paths(monkeypatch):
+    """FRA_REQUIRE_WAVE=1 fails a plan outside the wave kernel's scope (level 8), so the tests above prove the
+    wave kernel ran."""
+    monkeypatch.setenv("FRA_REQUIRE_WAVE", "1")
+    r = synth_window(4, 3, 1, 64, 256)
+    with pytest.raises(N.NativeError):
+        N.encode_windows(r, [(0, 0, 64, 256)], level=8, norm=16)
 
 
 @pytest.mark.parametrize("kind,bands,tile", [(4, 4, 1024), (3, 1, 512)])
@@ -289,7 +305,7 @@ def _noise_then_smooth(n_frames=3, seed=5):
 
 
 @pytest.mark.parametrize("level", [3, 5])
-def test_wave_kernel_noise_verbatim(level):
+def test_wave_kernel_noise_verbatim(require_wave, level):
     """Full-range noise: k_analyze_w's kept LPC winner is not smaller than VERBATIM, so the wave reloads the
     samples and writes VERBATIM from them (no hand-back); mixed with smooth bands in the same frames."""
     rng = np.random.default_rng(11 + level)
@@ -305,7 +321,7 @@ def test_wave_kernel_incompressible_start(level):
     check_windows(r, [(0, 0, r.shape[1], 4096)], level, 16)
 
 
-def test_wave_kernel_constant_and_two_valued():
+def test_wave_kernel_constant_and_two_valued(require_wave):
     """Constant frames (CONSTANT subframes), two-valued frames and their mix in one stream."""
     base = synth_window(3, 11, 1, 64, 192)[0].astype(np.int64)
     x = np.empty((1, 64 * 3, 192), np.int16)

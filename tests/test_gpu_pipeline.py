@@ -133,6 +133,83 @@ def test_corrupt_geotiff_fails_cleanly_while_encoding(tmp_path):
     assert not (tmp_path / "x.flac").exists()
 
 
+def _band_rows(r, wins, level, norm):
+    plan = N.Plan(N.default_context(0), None, False, r.dtype, r.shape[0], (r.shape[1] * r.shape[2], r.shape[2], 1),
+                  wins, level, 4096, norm)
+    try:
+        return plan.host_band_rows()
+    finally:
+        plan.close()
+
+
+@pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm,step,extra", [
+    (4, 4, 3600, 2200, 512, np.uint16, 5, 16, 512, 0),     # minimum ring (one band + one step): wraps every band
+    (4, 2, 3000, 1900, 256, np.uint16, 5, 16, 96, 37),     # steps that straddle band edges, odd ring size
+    (5, 3, 2600, 1500, 512, np.float32, 8, 24, 0, 0),      # 32-bps, default ring (two bands + a step)
+])
+def test_ring_encode_equals_device_path(kind, bands, H, W, tile, dtype, level, norm, step, extra):
+    """fra_plan_encode_ring: the raster only ever exists as a ring of a few row bands (the producer writes
+    image row r at ring row r % R once the encoder's H2D copies released it); frames and stream table equal
+    the device-resident path's, so no ring row was overwritten before its copy completed."""
+    from flac_raster.tiles import encode_tiles_ring, streams_from  # noqa: F401
+
+    r = synth_window(kind, 77, bands, H, W).astype(dtype)
+    wins = calculate_tiles(H, W, tile)
+    di, df = _device_path(r, wins, level, norm)
+    band = _band_rows(r, wins, level, norm)
+    st = step or band
+    R = band + st + extra if extra or step else 0
+    calls = []
+
+    def fill(dst, r0, r1):
+        calls.append((r0, r1))
+        dst[...] = r[:, r0:r1, :]
+
+    infos, frames, ring_rows = N.encode_windows_ring(r.shape, r.dtype, wins, fill, level, 4096, norm, step=st,
+                                                     ring_rows=R)
+    assert ring_rows < H  # the raster was never whole in host memory
+    assert bytes(frames) == df and _table(infos) == _table(di)
+    assert calls[0][0] == 0 and calls[-1][1] == H and all(a[1] == b[0] for a, b in zip(calls, calls[1:]))
+
+
+def test_ring_geotiff_larger_than_ring_equals_device_path(tmp_path):
+    """The user path: create_streaming_flac on a GeoTIFF much taller than the ring (single device: the ring
+    path) -- container bytes equal the device-resident path's container."""
+    from flac_raster.streaming import encode_geotiff_ring
+    from flac_raster.tiff import GeoTIFF, write_geotiff
+
+    H, W, tile = 4200, 1800, 512
+    r = synth_window(4, 21, 3, H, W).astype(np.uint16)
+    p = tmp_path / "big.tif"
+    write_geotiff(p, r, compression="deflate", tile=256, predictor=2)
+    tiles = calculate_tiles(H, W, tile)
+    g = GeoTIFF(p)
+    try:
+        streams, R = encode_geotiff_ring(g, tiles, 5, 0, tile, ring_rows=_band_rows(r, tiles, 5, 16) + 512)
+    finally:
+        g.close()
+    assert R < H / 3
+    di, df = _device_path(r, tiles, 5, 16)
+    assert b"".join(bytes(s.body) for s in streams) == df
+    out = tmp_path / "s.flac"
+    create_streaming_flac(p, out, tile, 5)
+    ref = assemble_streaming(tiles, streams, r.shape, r.dtype, Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0), None, tile)
+    assert out.read_bytes() == ref
+
+
+def test_ring_producer_failure_is_reported():
+    r = synth_window(4, 5, 1, 3000, 1024).astype(np.uint16)
+    wins = calculate_tiles(3000, 1024, 512)
+
+    def fill(dst, r0, r1):
+        if r0 >= 1500:
+            raise OSError("decode failed")
+        dst[...] = r[:, r0:r1, :]
+
+    with pytest.raises(OSError):
+        N.encode_windows_ring(r.shape, r.dtype, wins, fill, 5, 4096, 16, step=256)
+
+
 def test_pinned_pool_reuse():
     a = N.pinned_empty(1 << 20, np.uint8)
     p = a.ctypes.data
