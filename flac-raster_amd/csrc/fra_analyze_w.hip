@@ -624,7 +624,8 @@ k_analyze_w(JobArgs a, int src) {
       const int dwi = lane < 24 ? lane >> 3 : (lane - 24) & 3;
       const int ow = (int)bperm32((uint32_t)o_l, 16 * dwi);
       const int L = 16 * dwi + ow;
-      const uint32_t info = (uint32_t)qsh | ((ow > 0 && ok) ? (uint32_t)lo << 8 : 0u);
+      // (computed at the SOURCE lane 16 wi + o_wi from its own values: its order o_l == lo there)
+      const uint32_t info = (uint32_t)qsh | ((o_l > 0 && ok) ? (uint32_t)o_l << 8 : 0u);
       const uint32_t vinfo = bperm32(info, L);
 #pragma unroll
       for (int jx = 0; jx < 8; jx++) {

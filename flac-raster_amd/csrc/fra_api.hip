@@ -76,6 +76,7 @@ struct fra_plan {
   fra_ctx* ctx = nullptr;
   fra_job job{};
   std::vector<fra_window> windows;
+  std::vector<int32_t> franges;  // fra_plan_create_ranged: [2 w] first frame, [2 w + 1] count (-1: to the end)
   std::vector<StreamDev> streams;
   std::vector<FrameDev> frames;
   int src = 0;
@@ -472,7 +473,14 @@ static int plan_build(fra_plan* p) {
     st.first_frame = (int32_t)nf_total;
     st.frame_number0 = (uint32_t)j.first_frame;
     st.ms = ms ? 1 : 0;
-    const int64_t nfr = (st.nsamples + j.blocksize - 1) / j.blocksize;
+    const int64_t nfr_all = (st.nsamples + j.blocksize - 1) / j.blocksize;
+    // frame range of this window (fra_plan_create_ranged): frames [fa, fa + nfr) of its stream; the
+    // normalisation still spans the whole window, frame numbers stay those of the whole stream
+    int64_t fa = 0, nfr = nfr_all;
+    if (!p->franges.empty()) {
+      fa = std::min<int64_t>(p->franges[2 * w], nfr_all);
+      nfr = p->franges[2 * w + 1] < 0 ? nfr_all - fa : std::min<int64_t>(p->franges[2 * w + 1], nfr_all - fa);
+    }
     st.nframes = (int32_t)nfr;
     if (st.nsamples > 0) {
       int64_t ext = st.base_off + (int64_t)(j.channels - 1) * j.band_stride + (int64_t)(wd.height - 1) * j.row_stride +
@@ -481,7 +489,7 @@ static int plan_build(fra_plan* p) {
       const int segs = (wd.width + 4095) / 4096;
       p->max_segs = (int)std::max<int64_t>(p->max_segs, (int64_t)segs * wd.height);
     }
-    for (int64_t f = 0; f < nfr; f++) {
+    for (int64_t f = fa; f < fa + nfr; f++) {
       FrameDev fr{};
       fr.stream = w;
       fr.index = (int32_t)f;
@@ -834,7 +842,15 @@ int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
   return FRA_OK;
 }
 
+static int plan_create(fra_ctx* ctx, const fra_job* job, const int32_t* franges, fra_plan** out);
 int fra_plan_create(fra_ctx* ctx, const fra_job* job, fra_plan** out) {
+  return plan_create(ctx, job, nullptr, out);
+}
+int fra_plan_create_ranged(fra_ctx* ctx, const fra_job* job, const int32_t* frame_ranges, fra_plan** out) {
+  if (!frame_ranges) return set_err(FRA_E_INVALID, "null frame_ranges");
+  return plan_create(ctx, job, frame_ranges, out);
+}
+static int plan_create(fra_ctx* ctx, const fra_job* job, const int32_t* franges, fra_plan** out) {
   if (!ctx || !job || !out) return set_err(FRA_E_INVALID, "null argument");
   if (job->channels < 1 || job->channels > 8) return set_err(FRA_E_INVALID, "channels must be 1..8 (got %d)", job->channels);
   if (job->blocksize < 16 || job->blocksize > kMaxBlock)
@@ -857,6 +873,14 @@ int fra_plan_create(fra_ctx* ctx, const fra_job* job, fra_plan** out) {
   p->job = *job;
   p->windows.assign(job->windows, job->windows + job->nwindows);
   p->job.windows = p->windows.data();
+  if (franges) {
+    for (int w = 0; w < job->nwindows; w++)
+      if (franges[2 * w] < 0) {
+        delete p;
+        return set_err(FRA_E_INVALID, "window %d: first frame %d < 0", w, franges[2 * w]);
+      }
+    p->franges.assign(franges, franges + 2 * (size_t)job->nwindows);
+  }
   int rc = plan_build(p);
   if (rc == FRA_OK && job->raster) rc = fra_plan_set_raster(p, job->raster, job->raster_on_device);
   if (rc != FRA_OK) {
@@ -926,7 +950,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   // else beside k_analyze_w on the side stream
   const bool wave = wave_path(p);
   // (tests: FRA_REQUIRE_WAVE=1 makes a plan that would not take the wave path fail instead)
-  static const bool require_wave = getenv("FRA_REQUIRE_WAVE") && atoi(getenv("FRA_REQUIRE_WAVE")) == 1;
+  const bool require_wave = getenv("FRA_REQUIRE_WAVE") && atoi(getenv("FRA_REQUIRE_WAVE")) == 1;
   if (require_wave && !wave && nf > 0) return set_err(FRA_E_STATE, "FRA_REQUIRE_WAVE: the plan does not take k_analyze_w");
   const auto plo = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f0 * 8);
   const auto phi = std::lower_bound(p->h_part.begin(), p->h_part.end(), gr.f1 * 8);

@@ -150,8 +150,9 @@ def load():
         L.fra_host_unregister.argtypes = [vp]
         L.fra_tiff_decode.argtypes = [vp, u64, C.POINTER(TiffLayout), C.POINTER(TiffChunk), i32, vp, i32]
         L.fra_plan_encode_host_progress.argtypes = [vp, vp, vp, u64, C.POINTER(u64), vp]
-        L.fra_plan_encode_ring.argtypes = [vp, vp, C.c_int64, vp, u64, C.POINTER(u64), vp, vp]
-        L.fra_plan_host_band_rows.argtypes = [vp, C.POINTER(C.c_int64)]
+        if hasattr(L, "fra_plan_encode_ring"):  # (r05; older builds load for same-box A/Bs)
+            L.fra_plan_encode_ring.argtypes = [vp, vp, C.c_int64, vp, u64, C.POINTER(u64), vp, vp]
+            L.fra_plan_host_band_rows.argtypes = [vp, C.POINTER(C.c_int64)]
         L.fra_tiff_compress_bound.argtypes = [i32, u64]
         L.fra_tiff_compress_bound.restype = u64
         L.fra_tiff_compress.argtypes = [i32, i32, vp, u64, i32, vp, u64, C.POINTER(u64), i32]

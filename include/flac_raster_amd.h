@@ -105,6 +105,13 @@ FRA_API void fra_ctx_destroy(fra_ctx *ctx);
 
 /* Plan = all device workspace for one job shape; execute enqueues only (no allocation/sync). */
 FRA_API int fra_plan_create(fra_ctx *ctx, const fra_job *job, fra_plan **out);
+/* The same plan over FRAME RANGES of the windows (r05, multi-GPU work items of equal size):
+ * frame_ranges[2 w] = first frame, frame_ranges[2 w + 1] = frame count (-1: to the stream's end) of window
+ * w.  The normalisation (data_min/max, sample rate) still spans the whole window and the frames keep their
+ * frame numbers, so the concatenated frames of all ranges of one window, in order, are exactly the stream
+ * fra_plan_create would encode (the reference encodes a window as one stream, cli.py:553-597).
+ * fra_stream_info.nframes / frame_bytes describe the range. */
+FRA_API int fra_plan_create_ranged(fra_ctx *ctx, const fra_job *job, const int32_t *frame_ranges, fra_plan **out);
 FRA_API int fra_plan_set_raster(fra_plan *plan, const void *raster, int32_t raster_on_device);
 FRA_API int fra_plan_execute(fra_plan *plan);
 FRA_API int fra_plan_sync(fra_plan *plan);

@@ -33,7 +33,7 @@ def test_distributed_gpu_container_equals_single_process(tmp_path, world, dtype,
     kind = 4 if dtype == np.uint16 else 5
     r = synth_window(kind, 31, 3, 1800, 1500).astype(dtype)
     src = tmp_path / "scene.tif"
-    write_geotiff(src, r, compression="deflate", tile=256, predictor=2 if dtype == np.uint16 else 3,
+    write_geotiff(src, r, compression="deflate", tile=256, predictor=2 if dtype == np.uint16 else 1,
                   transform=(10.0, 0.0, 300000.0, 0.0, -10.0, 5000040.0), crs="EPSG:32633")
     out = tmp_path / "dist.flac"
     port = _free_port()

@@ -143,9 +143,9 @@ def _band_rows(r, wins, level, norm):
 
 
 @pytest.mark.parametrize("kind,bands,H,W,tile,dtype,level,norm,step,extra", [
-    (4, 4, 3600, 2200, 512, np.uint16, 5, 16, 512, 0),     # minimum ring (one band + one step): wraps every band
-    (4, 2, 3000, 1900, 256, np.uint16, 5, 16, 96, 37),     # steps that straddle band edges, odd ring size
-    (5, 3, 2600, 1500, 512, np.float32, 8, 24, 0, 0),      # 32-bps, default ring (two bands + a step)
+    (4, 4, 4608, 2048, 512, np.uint16, 5, 16, 512, 0),     # minimum ring (one band + one step): wraps every band
+    (4, 2, 4608, 1900, 256, np.uint16, 5, 16, 96, 37),     # steps that straddle band edges, odd ring size
+    (5, 3, 4096, 2048, 512, np.float32, 8, 24, 0, 0),      # 32-bps, default ring (two bands + a step)
 ])
 def test_ring_encode_equals_device_path(kind, bands, H, W, tile, dtype, level, norm, step, extra):
     """fra_plan_encode_ring: the raster only ever exists as a ring of a few row bands (the producer writes
@@ -178,7 +178,7 @@ def test_ring_geotiff_larger_than_ring_equals_device_path(tmp_path):
     from flac_raster.streaming import encode_geotiff_ring
     from flac_raster.tiff import GeoTIFF, write_geotiff
 
-    H, W, tile = 4200, 1800, 512
+    H, W, tile = 6144, 1536, 512  # >= 2,048 frames: one tile row per host band
     r = synth_window(4, 21, 3, H, W).astype(np.uint16)
     p = tmp_path / "big.tif"
     write_geotiff(p, r, compression="deflate", tile=256, predictor=2)
