@@ -369,6 +369,9 @@ def main():
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="time rank R's LPT share of the scene for an N-GPU strong-scaling run, on this one GPU "
                          "(projection of the multi-GPU step; DESIGN.md section 7)")
+    ap.add_argument("--split", default="frames", choices=["frames", "lpt"],
+                    help="strong scaling: (tile, frame range) work items of equal frame count per rank (default; "
+                         "fra_plan_create_ranged) or whole tiles by LPT")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
     ap.add_argument("--no-trace", action="store_true", help="skip the in-run rocprofv3 kernel-trace pass")
@@ -429,12 +432,21 @@ def main():
         if world != 1 or not 0 <= sr < sn:
             raise SystemExit("--shard R/N needs a single process and 0 <= R < N")
         shard_of = (sr, sn)
-    owner = ([rank] * len(wins) if weak else lpt_shard(wins, world)) if shard_of is None else lpt_shard(wins, shard_of[1])
+    nparts = shard_of[1] if shard_of is not None else (1 if weak else world)
     if shard_of is not None:
         rank = shard_of[0]
-    mine = [i for i in range(len(wins)) if owner[i] == rank]
+    if args.split == "frames" or nparts == 1:
+        from flac_raster.tiles import frame_split
+        items = frame_split(wins, nparts)[rank if nparts > 1 else 0]
+    else:
+        owner = lpt_shard(wins, nparts)
+        items = [(i, 0, -(-(wins[i][2] * wins[i][3]) // 4096)) for i in range(len(wins)) if owner[i] == rank]
+    mine = [i for i, _, _ in items]
     my_wins = [wins[i] for i in mine]
-    plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"])
+    full = all(f0 == 0 and n * 4096 >= wins[i][2] * wins[i][3] for i, f0, n in items)
+    ranges = None if full else [(f0, n) for _, f0, n in items]
+    plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"],
+                  frame_ranges=ranges)
 
     if args.child:  # rocprofv3 child: the plan's launches only
         if args.child_serial:  # the roofline's mode: serial executes, each kernel alone on the device
@@ -466,7 +478,8 @@ def main():
     kms, nexec = plan.timing()
     plan.enable_timing(False)
     infos, total = plan.result()
-    my_px = sum(w[2] * w[3] for w in my_wins)
+    # pixels of this rank's frames (a partial tile counts its frame range only)
+    my_px = sum(min(wins[i][2] * wins[i][3], (f0 + n) * 4096) - f0 * 4096 for i, f0, n in items)
     my_in_bytes = my_px * B * dt.itemsize
     per_launch_ms = [k / max(1, nexec) for k in kms]
     ranks = allgather([dt_s, per_launch_ms[1], sum(per_launch_ms), len(my_wins), my_px, total])

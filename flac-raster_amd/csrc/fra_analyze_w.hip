@@ -233,10 +233,31 @@ __device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, i
 // element size only: the table index is the raw bit pattern (lut_index), the same for u8/i8 and u16/i16.
 // The row walk adds the uniform step = qs w + rs per vector (col < w, so at most one more wrap): no
 // division per vector for any width (a per-vector division was 14 KiB of this kernel's code)
+// FRA_W_ARITH (A/B knob): 0 every sample through the table; 1 every sample by normalize_to_audio's f64 op
+// sequence in registers (norm_sample: the table's own entries, so bit-identical) -- 9 VALU per sample instead of
+// a gather; 2 the odd vectors arithmetic, the even ones gathered
+#ifndef FRA_W_ARITH
+#define FRA_W_ARITH 0
+#endif
+struct WNorm {
+  double two_mn, range, rcp;  // (-2 mn: the exact 2 (x - mn) as one fma)
+  uint32_t flip;               // 0x8000 / 0x80: signed raster (raw bits -> value by (r ^ flip) - flip)
+};
+template <typename T>
+__device__ __forceinline__ int32_t wnorm(uint32_t r, const WNorm& q) {
+  const int32_t v = (int32_t)((r ^ q.flip) - q.flip);
+  const double t = fma((double)v, 2.0, q.two_mn);  // 2 (x - mn), exact
+  const double q0 = t * q.rcp;                     // Markstein: the correctly rounded t / range
+  const double rr = fma(-q0, q.range, t);
+  double u = fma(rr, q.rcp, q0);
+  u = u - 1.0;
+  u = u * 32767.0;
+  return (int32_t)u;  // (in [-32767, 32767]: the clamps of norm_sample never act on the tile's own values)
+}
 template <typename T>
 __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st, const FrameDev& fr, int c,
                                           const int32_t* lut, uint32_t* sw, int lane, uint32_t& orv, int32_t& vmin,
-                                          int32_t& vmax, bool stamp) {
+                                          int32_t& vmax, bool stamp, const WNorm& wn) {
   constexpr int V = 8 / (int)sizeof(T);
   constexpr int NV = kMaxBlock / 64 / V;
   constexpr uint32_t step = 64 * V;
@@ -266,8 +287,9 @@ __device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st,
 #pragma unroll
   for (int kv = 0; kv < NV; kv++) {
     int32_t g[V];
+    const bool arith = FRA_W_ARITH == 1 || (FRA_W_ARITH == 2 && (kv & 1));
 #pragma unroll
-    for (int e = 0; e < V; e++) g[e] = lut[(uint32_t)x[kv].v[e]];
+    for (int e = 0; e < V; e++) g[e] = arith ? wnorm<T>((uint32_t)x[kv].v[e], wn) : lut[(uint32_t)x[kv].v[e]];
     const int i = (lane + 64 * kv) * V;
 #pragma unroll
     for (int h = 0; h < V / 4; h++) {
@@ -333,7 +355,11 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
 
 // (no L2 prefetch of a later wave's rows, unlike k_analyze: measured slower here at every distance,
 // profiles/r04_ab_wave_prefetch_distance.txt)
-template <int MAXLAG>
+// PCAP: the level's max partition order (levels 3-4: 4, 5: 5, 6: 6) as a template argument (r05): full frames
+// always search orders PCAP..0 (4096 >> 7 > 8 = max order), so the group / node loops of the FIXED sums, the LPC
+// sums and the partition search are straight code instead of uniform branches on a runtime order -- branches
+// that also split the blocks the scheduler could otherwise overlap the ds_bpermute round trips in
+template <int MAXLAG, int PCAP>
 // occupancy target: 8 KiB of LDS lets 20 waves share a CU; <= 96 VGPRs make it 5 per SIMD
 #ifndef FRA_W_WAVES
 #define FRA_W_WAVES 5
@@ -343,7 +369,7 @@ template <int MAXLAG>
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FRA_W_WAVES, FRA_W_WAVES_MAX)))
 k_analyze_w(JobArgs a, int src) {
-  static_assert(MAXLAG == 8, "levels 3-6");
+  static_assert(MAXLAG == 8 && PCAP >= 4 && PCAP <= 6, "levels 3-6");
   __shared__ WaveSmem S;
   uint32_t* const sw = S.sw;
   const int lane = (int)threadIdx.x;
@@ -373,9 +399,17 @@ k_analyze_w(JobArgs a, int src) {
   // (the lambdas capture these locals, not the kernel arguments: taking the arguments' address costs registers)
   const void* const raster = a.raster;
   const int32_t* const lut = a.lut + (int64_t)fr.stream * a.lut_stride;
+  WNorm wn{};
+  if (FRA_W_ARITH) {
+    const NormParams np = norm_params(st, a.norm[fr.stream]);
+    wn.two_mn = -2.0 * np.mn;
+    wn.range = np.range;
+    wn.rcp = np.rcp;
+    wn.flip = src == ST_I16 ? 0x8000u : (src == ST_I8 ? 0x80u : 0u);
+  }
   auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx, bool first) {
-    if (src == ST_U8 || src == ST_I8) wload_lut<uint8_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first);  // uniform
-    else wload_lut<uint16_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first);
+    if (src == ST_U8 || src == ST_I8) wload_lut<uint8_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first, wn);  // uniform
+    else wload_lut<uint16_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first, wn);
   };
   load_samples(orv, vmin, vmax, true);
   orv = wave_or32(orv);
@@ -410,14 +444,14 @@ k_analyze_w(JobArgs a, int src) {
   wsync();
   const uint32_t hdr = 8u + (uint32_t)w;
   const uint32_t verb = hdr + (uint32_t)n * (uint32_t)sbps;
-  const int P = max_porder(n, 0, cfg.max_porder);  // = cfg.max_porder (3..6)
-  const int gsl = 8 - P;                             // lanes per finest partition: 2^gsl (chunks of 16)
+  constexpr int P = PCAP;                            // = max_porder(n, 0, cfg.max_porder)
+  constexpr int gsl = 8 - P;                         // lanes per finest partition: 2^gsl (chunks of 16)
   const int prec = qlp_precision(bps, n);
   const int lmax = cfg.max_lpc;                      // < n - 1
 
   // ---- 3a. FIXED residual sums (3.8) by finite differences, per finest partition: group sums of the lanes
   // of a partition, gathered so that lane p holds partition p (ds_bpermute from the group's last lane)
-  const int npl = 6 - gsl;  // log2 finest partitions per iteration
+  constexpr int npl = 6 - gsl;  // log2 finest partitions per iteration
   const int pj = lane >> npl;  // the iteration of partition `lane` (>= 4: lane >= 2^P, none)
   const int psrc = ((lane & ((1 << npl) - 1)) << gsl) | ((1 << gsl) - 1);  // its group's last lane
   uint32_t pfix[5] = {0, 0, 0, 0, 0};
@@ -525,7 +559,11 @@ k_analyze_w(JobArgs a, int src) {
             {
               const uint32_t* po = sw + 8 * lnw + kWIterDw * j;
               const uint4 v0 = lds4(po), v1 = lds4(po + 4), v2 = lds4(t == kWChunks - 1 ? po : po + 8);
-              const uint32_t dw[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+              // the last chunk's look-ahead (samples past n) is zero: its coefficients may then be read without
+              // a bound (the table has slack past its last row, plan_build), and every product is still +-0
+              const bool last = t == kWChunks - 1;
+              const uint32_t dw[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                       last ? 0u : v2.x, last ? 0u : v2.y, last ? 0u : v2.z, last ? 0u : v2.w};
 #pragma unroll
               for (int p = 0; p < (kChunk + MAXLAG) / 2; p++) {
                 y[2 * p] = lo16(dw[p]);
@@ -545,7 +583,8 @@ k_analyze_w(JobArgs a, int src) {
 #pragma unroll
                 for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = 1.0f;
               } else {
-                load_window<MAXLAG>(win, i0, n, wc);
+#pragma unroll
+                for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = win[i0 + jx];  // (no per-entry bound)
               }
 #pragma unroll
               for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = (float)y[jx] * wc[jx];
@@ -724,7 +763,7 @@ k_analyze_w(JobArgs a, int src) {
         }
       }
     }
-    const int pm = max_porder(n, o, cfg.max_porder);
+    constexpr int pm = P;  // max_porder(n, o, cfg.max_porder) == P for n = 4096, o <= 8
     uint64_t best;
     int bp;
     uint32_t kreg;
@@ -828,17 +867,46 @@ k_analyze_w(JobArgs a, int src) {
 #pragma unroll
     for (int j = 0; j < kWIters; j++) {
       const int t = 64 * j + lane;
-      uint32_t un[kChunk];
-      residuals(j, un, cyx);
       const int pidx = t >> tl;
       const int k0 = __shfl((int)wk, pidx & 63, 64);
       const int km = k0 > 0 ? k0 - 1 : 0;
       uint32_t f0 = 0, f1 = 0, f2 = 0;  // u < 2^28: 16 of them fit 32 bits
+      if constexpr (kept) {
+        // the kept residuals are u16 pairs: one v_pk_lshrrev_b16 + one v_dot2_u32_u16 (both halves times 1, into
+        // 32 bits) per pair and shift -- half the instructions of the per-sample shifts and adds
+        const uint32_t* po = sw + 8 * lane + kWIterDw * j;
+        // (a u16 shifted by >= 16 is 0: the shift is capped at 15 and the pair weighted 0 instead -- the hardware
+        // takes the shift count mod 16)
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        auto sh = [](int k) -> u16x2 {
+          const unsigned short c = (unsigned short)(k < 15 ? k : 15);
+          return u16x2{c, c};
+        };
+        auto wt = [](int k) -> u16x2 {
+          const unsigned short c = k < 16 ? 1 : 0;
+          return u16x2{c, c};
+        };
+        const u16x2 sm = sh(km), s0 = sh(k0), s1 = sh(k0 + 1), mm = wt(km), m0 = wt(k0), m1 = wt(k0 + 1);
 #pragma unroll
-      for (int jj = 0; jj < kChunk; jj++) {
-        f0 += un[jj] >> km;
-        f1 += un[jj] >> k0;
-        f2 += un[jj] >> (k0 + 1);
+        for (int p = 0; p < kChunk / 4; p++) {
+          const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
+          const u16x2 w0 = __builtin_bit_cast(u16x2, v.x), w1 = __builtin_bit_cast(u16x2, v.y);
+          f0 = __builtin_amdgcn_udot2(w0 >> sm, mm, f0, false);
+          f0 = __builtin_amdgcn_udot2(w1 >> sm, mm, f0, false);
+          f1 = __builtin_amdgcn_udot2(w0 >> s0, m0, f1, false);
+          f1 = __builtin_amdgcn_udot2(w1 >> s0, m0, f1, false);
+          f2 = __builtin_amdgcn_udot2(w0 >> s1, m1, f2, false);
+          f2 = __builtin_amdgcn_udot2(w1 >> s1, m1, f2, false);
+        }
+      } else {
+        uint32_t un[kChunk];
+        residuals(j, un, cyx);
+#pragma unroll
+        for (int jj = 0; jj < kChunk; jj++) {
+          f0 += un[jj] >> km;
+          f1 += un[jj] >> k0;
+          f2 += un[jj] >> (k0 + 1);
+        }
       }
       fk[j][0] = f0;
       fk[j][1] = f1;
@@ -851,23 +919,26 @@ k_analyze_w(JobArgs a, int src) {
         v0 = group_sum64(f0, ls); v1 = group_sum64(f1, ls); v2 = group_sum64(f2, ls);
       }
       if (tl <= 6) {  // the partition lies inside this iteration: its last lane decides
+        // (evaluated on every lane -- no exec masking -- and kept on the partition's last lane)
+        const uint32_t cnt = (uint32_t)(pz - (pidx == 0 ? o : 0));
+        const uint64_t ev[3] = {v0, v1, v2};
+        uint64_t best = 0;
         int bk = 0;
-        if ((lane & ((1 << ls) - 1)) == (1 << ls) - 1) {
-          const uint64_t cnt = (uint64_t)(pz - (pidx == 0 ? o : 0));
-          const uint64_t ev[3] = {v0, v1, v2};
-          uint64_t best = 0;
-          bool first = true;
+        bool first = true;
 #pragma unroll
-          for (int dk = -1; dk <= 1; dk++) {
-            const int kk = k0 + dk;
-            if (kk < 0 || kk > 30) continue;
-            const uint64_t e = cnt * (uint64_t)(kk + 1) + ev[dk + 1];
-            if (first || e < best) { best = e; bk = kk; first = false; }
-          }
-          bitsl += (uint32_t)best;
-          bigl = bigl || bk > 14;
-          d->k[pidx] = (uint8_t)bk;
+        for (int dk = -1; dk <= 1; dk++) {
+          const int kk = k0 + dk;
+          const uint64_t e = (uint64_t)(cnt * (uint32_t)(kk + 1)) + ev[dk + 1];
+          const bool take = kk >= 0 && kk <= 30 && (first || e < best);
+          best = take ? e : best;
+          bk = take ? kk : bk;
+          first = first && !(kk >= 0 && kk <= 30);
         }
+        const bool leader = (lane & ((1 << ls) - 1)) == (1 << ls) - 1;
+        bk = leader ? bk : 0;
+        bitsl += leader ? (uint32_t)best : 0u;
+        bigl = bigl || bk > 14;
+        if (leader) d->k[pidx] = (uint8_t)bk;
         kc[j] = (uint32_t)__shfl(bk, lane | ((1 << ls) - 1), 64);
       } else {  // ps <= 1: whole-iteration sums accumulate into the partition's running sums (uniform)
         auto rl64 = [](uint64_t v) -> uint64_t {
@@ -1006,13 +1077,13 @@ k_analyze_w(JobArgs a, int src) {
       if (pstart) { lds_put(buf, p, kcur, pb); p += (uint32_t)pb; }
       // Rice code (stop bit + kcur low bits) left-aligned: bit 31 = the stop bit
       const uint32_t sal = 31u - kcur;
+      // (warm-up positions -- lane 0 of iteration 0 -- OR nothing and do not advance: selects, not a branch)
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
-        if (!(jj < 12 && head && jj < o)) {
-          const uint32_t Pp = p + (un[jj] >> kcur);
-          lds_put_al(buf, Pp, (un[jj] << sal) | 0x80000000u);
-          p = Pp + 1u + kcur;
-        }
+        const bool skip = jj < 12 && head && jj < o;
+        const uint32_t Pp = p + (un[jj] >> kcur);
+        lds_put_al(buf, Pp, skip ? 0u : ((un[jj] << sal) | 0x80000000u));
+        p = skip ? p : Pp + 1u + kcur;
       }
     };
     uint32_t cye[6] = {0, 0, 0, 0, 0, 0};
@@ -1075,7 +1146,11 @@ hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStr
   const dim3 grid((unsigned)a.frame_count, (unsigned)cw);
   const LevelCfg cfg = level_cfg(level);
   if (cfg.nsub == 0 || cfg.max_lpc > 8) return hipErrorInvalidValue;  // levels 3-6 only
-  k_analyze_w<8><<<grid, 64, 0, s>>>(a, src);
+  switch (cfg.max_porder) {
+    case 4: k_analyze_w<8, 4><<<grid, 64, 0, s>>>(a, src); break;
+    case 5: k_analyze_w<8, 5><<<grid, 64, 0, s>>>(a, src); break;
+    default: k_analyze_w<8, 6><<<grid, 64, 0, s>>>(a, src); break;
+  }
   return hipGetLastError();
 }
 

@@ -568,7 +568,9 @@ static int plan_build(fra_plan* p) {
   HIPCHK(hipMalloc(&p->d_out, p->out_cap));
   const size_t wn = (size_t)std::max<size_t>(1, win_sizes.size()) * std::max(1, p->nwin) * j.blocksize;
   // exact size: k_analyze reads entries [0, n) of the table of block size n only (load_window)
-  std::vector<float> wt(wn, 0.0f);
+  // + slack: k_analyze_w reads a whole chunk's look-ahead of coefficients without a bound (its samples past n
+  // are zero), which may run 16 + MAXLAG entries past the last row
+  std::vector<float> wt(wn + 64, 0.0f);
   for (size_t t = 0; t < win_sizes.size(); t++)
     window_set(wt.data() + t * std::max(1, p->nwin) * j.blocksize, win_sizes[t], j.blocksize, nsub);
   HIPCHK(hipMalloc(&p->d_win, sizeof(float) * wt.size()));

@@ -588,10 +588,13 @@ __device__ __forceinline__ void rice_pick(uint64_t n, uint64_t S, int& k_out, ui
 // the same pick in 32-bit arithmetic, valid (bit-identical) whenever S < 2^29 and n < 2^13: then
 // kc <= bitlen(S) - bitlen(n) + 1, so n * 2^k < 2^31 for every candidate k <= kc + 1, 2S < 2^30, and no
 // intermediate wraps; n * (2^k - 1) as (n << k) - n, n * (k + 1) on the 24-bit multiplier
+// Branch-free (r05): the <= 4 candidates lo .. lo + 3 (hi - lo <= 3) are all evaluated and the ones past hi
+// masked, so lanes with different ranges run one straight instruction stream (the loop with a per-lane trip
+// count ran under exec masking: ~3 SALU per trip plus the loop's own branches); same first-minimum rule.
 __device__ __forceinline__ void rice_pick32(uint32_t n, uint32_t S, int& k_out, uint32_t& bits_out) {
   const int a = S ? 32 - __clz((int)S) : 0, b = n ? 32 - __clz((int)n) : 0;
   int kc = a > b ? a - b : 0;
-  if (S >= (n << kc)) kc++;
+  kc += S >= (n << kc) ? 1 : 0;
   const int lo = kc - 2 < 0 ? 0 : kc - 2, hi = kc + 1 > 30 ? 30 : kc + 1;
   auto est = [&](int k) -> uint32_t {
     const uint32_t l = (n << k) - n;
@@ -600,9 +603,13 @@ __device__ __forceinline__ void rice_pick32(uint32_t n, uint32_t S, int& k_out, 
   };
   uint32_t best = est(lo);
   int bk = lo;
-  for (int k = lo + 1; k <= hi; k++) {
-    const uint32_t e = est(k);
-    if (e < best) { best = e; bk = k; }
+#pragma unroll
+  for (int dk = 1; dk <= 3; dk++) {
+    const int k = lo + dk;
+    const uint32_t e = est(k <= 30 ? k : 30);
+    const bool take = k <= hi && e < best;
+    best = take ? e : best;
+    bk = take ? k : bk;
   }
   k_out = bk;
   bits_out = best;
@@ -1018,9 +1025,14 @@ __device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, in
     FRA_NODE_STEP32(0) FRA_NODE_STEP32(1) FRA_NODE_STEP32(2)
     FRA_NODE_STEP32(3) FRA_NODE_STEP32(4) FRA_NODE_STEP32(5)
 #undef FRA_NODE_STEP32
-    if (lane >= 1 && p <= P && p <= pm) {
-      rice_pick32((uint32_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits32);
-      big = kn > 14;
+    {  // every lane (no exec masking), the result kept where the lane holds a node of a searched level
+      int kq;
+      uint32_t bq;
+      rice_pick32((uint32_t)((n >> p) - (jn == 0 ? o : 0)), nv, kq, bq);
+      const bool act = lane >= 1 && p <= P && p <= pm;
+      kn = act ? kq : 0;
+      bits32 = act ? bq : 0u;
+      big = act && kq > 14;
     }
     if (P == 6 && pm == 6) {  // level 6: the finest sums at lane j
       uint32_t b6;
@@ -1069,12 +1081,19 @@ __device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, in
   v += dpp32<DPP_BC15, 0xA>(v);
   tot[5] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
   tot[6] = tot6;
+  // orders pm .. 0, '<=' keeps the smaller order: unrolled over the compile-time order so tot[q] and the
+  // masks are plain registers (a runtime q compiled to a select chain over tot[] per step, ~40 SALU each)
   uint64_t best = 0;
   int bp = pm;
-  for (int q = pm; q >= 0; q--) {
-    const bool bq = q == 6 ? big6 : ((bigm >> (1u << q)) & ((1ull << (1u << q)) - 1)) != 0;
-    const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
-    if (q == pm || t <= best) { best = t; bp = q; }
+  bool first = true;
+#pragma unroll
+  for (int q = 6; q >= 0; q--) {
+    if (q <= pm) {
+      const bool bq = q == 6 ? big6 : ((bigm >> (1u << (q % 6))) & ((1ull << (1u << (q % 6))) - 1)) != 0;
+      const uint64_t t = (uint64_t)tot[q] + (uint64_t)(1u << q) * (bq ? 5 : 4) + 6;
+      if (first || t <= best) { best = t; bp = q; }
+      first = false;
+    }
   }
   best_out = best;
   bp_out = bp;

@@ -93,7 +93,7 @@ EXPORTS = [
     "fra_decode", "fra_plan_encode_host", "fra_plan_capacity", "fra_host_alloc", "fra_host_free",
     "fra_host_register", "fra_host_unregister", "fra_tiff_decode", "fra_plan_set_first_frame",
     "fra_plan_flags", "fra_plan_encode_host_progress", "fra_tiff_compress_bound", "fra_tiff_compress",
-    "fra_plan_encode_ring", "fra_plan_host_band_rows",
+    "fra_plan_encode_ring", "fra_plan_host_band_rows", "fra_plan_create_ranged",
 ]
 
 
@@ -150,7 +150,9 @@ def load():
         L.fra_host_unregister.argtypes = [vp]
         L.fra_tiff_decode.argtypes = [vp, u64, C.POINTER(TiffLayout), C.POINTER(TiffChunk), i32, vp, i32]
         L.fra_plan_encode_host_progress.argtypes = [vp, vp, vp, u64, C.POINTER(u64), vp]
-        if hasattr(L, "fra_plan_encode_ring"):  # (r05; older builds load for same-box A/Bs)
+        if hasattr(L, "fra_plan_create_ranged"):  # (r05; older builds load for same-box A/Bs)
+            L.fra_plan_create_ranged.argtypes = [vp, C.POINTER(Job), C.POINTER(C.c_int32), C.POINTER(vp)]
+        if hasattr(L, "fra_plan_encode_ring"):
             L.fra_plan_encode_ring.argtypes = [vp, vp, C.c_int64, vp, u64, C.POINTER(u64), vp, vp]
             L.fra_plan_host_band_rows.argtypes = [vp, C.POINTER(C.c_int64)]
         L.fra_tiff_compress_bound.argtypes = [i32, u64]
@@ -326,7 +328,11 @@ class Plan:
 
     def __init__(self, ctx: Context, raster_ptr: Optional[int], on_device: bool, dtype: np.dtype, channels: int,
                  strides: Tuple[int, int, int], windows: Sequence[Tuple[int, int, int, int]], level: int = 5,
-                 blocksize: int = 4096, norm: int = 16, sample_rate: int = 0, keepalive=None):
+                 blocksize: int = 4096, norm: int = 16, sample_rate: int = 0, keepalive=None,
+                 frame_ranges: Optional[Sequence[Tuple[int, int]]] = None):
+        """``frame_ranges``: per window (first frame, count; count -1 = to the end) -- the plan encodes only
+        those frames of each window's stream (``fra_plan_create_ranged``; normalisation over the whole
+        window, frame numbers of the whole stream)."""
         L = load()
         self.ctx = ctx
         self.nwin = len(windows)
@@ -345,7 +351,13 @@ class Plan:
         job.norm = norm
         job.sample_rate = sample_rate
         h = C.c_void_p()
-        _check(L.fra_plan_create(ctx.h, C.byref(job), C.byref(h)))
+        if frame_ranges is None:
+            _check(L.fra_plan_create(ctx.h, C.byref(job), C.byref(h)))
+        else:
+            if len(frame_ranges) != self.nwin:
+                raise ValueError("one (first, count) frame range per window")
+            self._ranges = (C.c_int32 * max(2, 2 * self.nwin))(*[int(v) for fr in frame_ranges for v in fr])
+            _check(L.fra_plan_create_ranged(ctx.h, C.byref(job), self._ranges, C.byref(h)))
         self.h = h
 
     def set_raster(self, ptr: int, on_device: bool, keepalive=None):
@@ -525,14 +537,15 @@ def _element_strides(a: np.ndarray) -> Tuple[int, int, int]:
 
 def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize: int = 4096, norm: int = 16,
                           sample_rate: int = 0, device: int = 0, pinned: bool = True,
-                          rows_ready: Optional[np.ndarray] = None):
+                          rows_ready: Optional[np.ndarray] = None, frame_ranges=None):
     """Encode windows of a band-planar host raster ``(B, H, W)`` (any non-negative strides, e.g. a row
     band view of a larger raster) through the pipelined host path (``fra_plan_encode_host``).
 
     Returns ``(infos, frames)``: ``frames`` is a uint8 array (page-locked unless ``pinned=False``) with
     every window's FLAC frames concatenated in window order; ``infos[i].offset/.frame_bytes`` slice it.
     ``rows_ready``: the raster is still being filled by a producer thread that publishes the rows done
-    in ``rows_ready[0]`` (``fra_plan_encode_host_progress``).
+    in ``rows_ready[0]`` (``fra_plan_encode_host_progress``).  ``frame_ranges``: (first frame, count) per
+    window (``fra_plan_create_ranged``).
     """
     a = np.asarray(raster)
     if a.ndim == 2:
@@ -543,7 +556,8 @@ def encode_windows_buffer(raster: np.ndarray, windows, level: int = 5, blocksize
         a = a.astype(a.dtype.newbyteorder("="))
     B = a.shape[0]
     ctx = default_context(device)
-    plan = Plan(ctx, None, False, a.dtype, B, _element_strides(a), windows, level, blocksize, norm, sample_rate)
+    plan = Plan(ctx, None, False, a.dtype, B, _element_strides(a), windows, level, blocksize, norm, sample_rate,
+                frame_ranges=frame_ranges)
     try:
         cap, _ = plan.capacity()
         out = pinned_empty(cap, np.uint8) if pinned else np.empty(cap, np.uint8)

@@ -20,7 +20,7 @@ import tempfile
 from pathlib import Path
 from typing import Callable, List, Optional, Sequence, Tuple
 
-from .tiles import TileStream, encode_tiles, lpt_assign
+from .tiles import TileStream, encode_tiles, frame_split, frames_of, lpt_assign
 
 
 class Dist:
@@ -164,28 +164,53 @@ def read_rank_mosaic(src, windows: Sequence[Tuple[int, int, int, int]], pinned: 
             g.close()
 
 
+def rank_items(tiles: Sequence[Tuple[int, int, int, int]], world: int, rank: int,
+               split: str = "frames") -> List[Tuple[int, int, int]]:
+    """This rank's work items (tile index, first frame, frame count): ``split="frames"`` -- equal frame
+    counts per rank (``frame_split``: whole tiles plus at most a partial tile at each end, SURVEY.md 8(e)'s
+    (tile, frame-range) items); ``"lpt"`` -- whole tiles by LPT on pixel count."""
+    if split == "frames":
+        return frame_split(tiles, world)[rank]
+    return [(i, 0, frames_of(tiles[i])) for i in shard(tiles, world, rank)]
+
+
 def encode_tiles_distributed(raster, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,
                              d: Optional[Dist] = None, encode_fn: EncodeFn = encode_tiles,
-                             dst: int = 0) -> Optional[List[TileStream]]:
-    """Each rank encodes its LPT share on its local GPU; ``dst`` receives every stream in tile order
-    (other ranks get ``None``).  Bytes are identical for any world size.  ``raster`` is an in-memory
-    (bands, H, W) array, or a GeoTIFF path / ``GeoTIFF``: then every rank decodes only its own tiles'
-    windows (``read_rank_mosaic``), never the whole scene."""
+                             dst: int = 0, split: str = "frames") -> Optional[List[TileStream]]:
+    """Each rank encodes its work items (``rank_items``) on its local GPU; ``dst`` receives every stream in
+    tile order (other ranks get ``None``): the frames of a tile split over ranks are concatenated in frame
+    order, which is exactly the tile's stream.  Bytes are identical for any world size and split.
+    ``raster`` is an in-memory (bands, H, W) array, or a GeoTIFF path / ``GeoTIFF``: then every rank
+    decodes only the windows of its own tiles (``read_rank_mosaic``), never the whole scene.  ``encode_fn``
+    takes ``frame_ranges=`` when a rank holds part of a tile."""
     d = d or Dist()
-    mine = shard(tiles, d.world, d.rank)
+    items = rank_items(tiles, d.world, d.rank, split)
+    mine = [i for i, _, _ in items]
+    whole = all(f0 == 0 and n >= frames_of(tiles[i]) for i, f0, n in items)
+    kw = {} if whole else {"frame_ranges": [(f0, n) for _, f0, n in items]}
     if isinstance(raster, (str, os.PathLike)) or type(raster).__name__ == "GeoTIFF":
         mosaic, local = read_rank_mosaic(raster, [tiles[i] for i in mine], pinned=encode_fn is encode_tiles)
-        streams = encode_fn(mosaic, local, level, [d.local_rank]) if mine else []
+        streams = encode_fn(mosaic, local, level, [d.local_rank], **kw) if mine else []
         del mosaic
     else:
-        streams = encode_fn(raster, [tiles[i] for i in mine], level, [d.local_rank]) if mine else []
-    parts = d.gather_streams(list(zip(mine, streams)), dst)
+        streams = encode_fn(raster, [tiles[i] for i in mine], level, [d.local_rank], **kw) if mine else []
+    parts = d.gather_streams([((i, f0), ts) for (i, f0, _), ts in zip(items, streams)], dst)
     if d.rank != dst:
         return None
-    out: List[Optional[TileStream]] = [None] * len(tiles)
+    pieces: List[List[Tuple[int, TileStream]]] = [[] for _ in tiles]
     for part in parts:
-        for i, ts in part:
-            out[i] = ts
-    if any(ts is None for ts in out):
-        raise RuntimeError("a tile was not encoded by any rank")
-    return out  # type: ignore[return-value]
+        for (i, f0), ts in part:
+            pieces[i].append((f0, ts))
+    out: List[TileStream] = []
+    for i, ps in enumerate(pieces):
+        if not ps:
+            raise RuntimeError(f"tile {i} was not encoded by any rank")
+        ps.sort(key=lambda x: x[0])
+        if len(ps) == 1:
+            out.append(ps[0][1])
+            continue
+        head = ps[0][1]
+        body = b"".join(bytes(ts.body) for _, ts in ps)
+        out.append(TileStream(head.header, body, head.data_min, head.data_max, head.sample_rate, head.bps,
+                              head.channels, sum(ts.nframes for _, ts in ps)))
+    return out

@@ -50,6 +50,31 @@ def split_contiguous(weights: Sequence[int], parts: int) -> List[Tuple[int, int]
     return out
 
 
+def frames_of(tile: Tuple[int, int, int, int], blocksize: int = 4096) -> int:
+    """FLAC frames of one tile's stream."""
+    return -(-(tile[2] * tile[3]) // blocksize)
+
+
+def frame_split(tiles: Sequence[Tuple[int, int, int, int]], parts: int,
+                blocksize: int = 4096) -> List[List[Tuple[int, int, int]]]:
+    """Work items of equal size for ``parts`` ranks ((tile, frame range) items): the frames
+    of all tiles in tile order, cut into ``parts`` contiguous runs of equal frame count; part k gets a list
+    of (tile index, first frame, frame count) -- whole tiles, plus at most a partial tile at each end.  The
+    frames of one tile, concatenated over the parts in order, are that tile's stream."""
+    counts = [frames_of(t, blocksize) for t in tiles]
+    total = sum(counts)
+    cuts = [total * k // parts for k in range(parts + 1)]
+    out: List[List[Tuple[int, int, int]]] = [[] for _ in range(parts)]
+    base = 0
+    for i, n in enumerate(counts):
+        for k in range(parts):
+            a, b = max(base, cuts[k]), min(base + n, cuts[k + 1])
+            if b > a:
+                out[k].append((i, a - base, b - a))
+        base += n
+    return out
+
+
 def lpt_assign(weights: Sequence[int], parts: int) -> List[List[int]]:
     """Longest-processing-time assignment (used when data already lives on every device)."""
     order = sorted(range(len(weights)), key=lambda i: (-weights[i], i))
@@ -97,7 +122,7 @@ def norm_bits(dtype) -> int:
 
 
 def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int, device: int,
-                  norm: int, out: list, errors: list, slot: int, rows_ready=None):
+                  norm: int, out: list, errors: list, slot: int, rows_ready=None, frame_ranges=None):
     try:
         r0 = min(t[0] for t in tiles)
         r1 = max(t[0] + t[2] for t in tiles)
@@ -106,7 +131,8 @@ def _encode_group(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]]
         if rows_ready is not None and r0 != 0:
             raise ValueError("rows_ready needs the group to start at raster row 0")
         infos, frames = _native.encode_windows_buffer(sub, wins, level=level, blocksize=BLOCKSIZE, norm=norm,
-                                                      device=device, rows_ready=rows_ready)
+                                                      device=device, rows_ready=rows_ready,
+                                                      frame_ranges=frame_ranges)
         out[slot] = streams_from(infos, frames)
     except BaseException as e:  # re-raised on the calling thread
         errors.append(e)
@@ -139,13 +165,15 @@ def encode_tiles_ring(shape, dtype, tiles: Sequence[Tuple[int, int, int, int]], 
 
 def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]], level: int = 5,
                  devices: Optional[Sequence[int]] = None, rows_ready=None,
-                 producer: Optional[threading.Thread] = None) -> List[TileStream]:
+                 producer: Optional[threading.Thread] = None, frame_ranges=None) -> List[TileStream]:
     """Encode every tile of a band-planar ``(B, H, W)`` raster as its own FLAC stream on the GPU(s).
 
     Each stream equals what ``normalize_to_audio`` + ``pyflac.StreamEncoder(blocksize=4096)``
     produce for ``raster[:, r:r+h, c:c+w]`` interleaved pixel-major (``cli.py:557-597``).
     ``rows_ready`` / ``producer``: the raster is still being decoded by ``producer``, which publishes the
     rows done in ``rows_ready[0]``; one device encodes as the rows land, several wait for the producer.
+    ``frame_ranges``: (first frame, count) per tile -- only those frames of each stream (one device; the
+    multi-GPU work items of ``frame_split``); the TileStream's body then holds just those frames.
     """
     a = np.asarray(raster)
     if a.ndim == 2:
@@ -167,7 +195,11 @@ def encode_tiles(raster: np.ndarray, tiles: Sequence[Tuple[int, int, int, int]],
         if rows_ready[0] < 0:
             raise RuntimeError("raster decode failed")
         rows_ready = None
-    if len(runs) == 1:
+    if frame_ranges is not None:
+        if len(devs) != 1:
+            raise ValueError("frame_ranges: one device per call (one rank per GPU)")
+        _encode_group(a, tiles, level, devs[0], norm, out, errors, 0, rows_ready, frame_ranges)
+    elif len(runs) == 1:
         _encode_group(a, tiles, level, devs[0], norm, out, errors, 0, rows_ready)
     else:
         th = [threading.Thread(target=_encode_group, args=(a, tiles[s:e], level, devs[k], norm, out, errors, k))

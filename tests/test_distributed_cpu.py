@@ -29,7 +29,7 @@ def _raster():
     return (base - base.min()).astype(np.int16)
 
 
-def _worker(rank, world, port, out_dir, from_file=False):
+def _worker(rank, world, port, out_dir, from_file=False, tile=64, split="frames"):
     for p in (HERE.parent / "flac-raster_amd", HERE.parent / "oracle", HERE):
         sys.path.insert(0, str(p))
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -42,36 +42,61 @@ def _worker(rank, world, port, out_dir, from_file=False):
 
     d = Dist(backend="gloo")
     r = _raster()
-    tiles = calculate_tiles(200, 333, 64)
+    tiles = calculate_tiles(200, 333, tile)
     mine = shard(tiles, world, rank)
     assert d.allsum(len(mine)) == len(tiles)
     assert d.allmax(float(rank)) == float(world - 1)
     d.barrier()
     src = Path(out_dir, "scene.tif") if from_file else r  # file: each rank decodes only its own windows
-    streams = encode_tiles_distributed(src, tiles, 5, d, encode_fn=oracle_encode_tiles)
+    streams = encode_tiles_distributed(src, tiles, 5, d, encode_fn=oracle_encode_tiles, split=split)
     if rank == 0:
         blob = assemble_streaming(tiles, streams, r.shape, r.dtype, Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0),
-                                  "EPSG:3857", 64)
-        Path(out_dir, f"w{world}{'f' if from_file else ''}.bin").write_bytes(blob)
+                                  "EPSG:3857", tile)
+        Path(out_dir, f"w{world}{'f' if from_file else ''}_{tile}_{split}.bin").write_bytes(blob)
     else:
         assert streams is None
     d.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_container_identical(tmp_path, world):
+@pytest.mark.parametrize("world,tile,split", [(2, 64, "frames"), (3, 64, "lpt"), (3, 128, "frames"),
+                                              (2, 160, "frames")])
+def test_distributed_container_identical(tmp_path, world, tile, split):
+    """World 2/3, whole-tile LPT items and (tile, frame range) items: with tiles of 4-7 frames the equal
+    frame-count split cuts tiles between ranks, whose frame slices the writer joins back into streams."""
     sys.path.insert(0, str(HERE))
     from flac_raster.geo import Affine
     from flac_raster.streaming import assemble_streaming
-    from flac_raster.tiles import calculate_tiles
+    from flac_raster.tiles import calculate_tiles, frame_split
     from oracle_tiles import oracle_encode_tiles
 
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    tiles = calculate_tiles(200, 333, tile)
+    if tile > 64 and split == "frames":  # the split really cuts a tile
+        assert any(f0 > 0 for part in frame_split(tiles, world) for _, f0, _ in part)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), False, tile, split), nprocs=world, join=True)
     r = _raster()
-    tiles = calculate_tiles(200, 333, 64)
     ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, 5), r.shape, r.dtype,
-                             Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0), "EPSG:3857", 64)
-    assert (tmp_path / f"w{world}.bin").read_bytes() == ref
+                             Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0), "EPSG:3857", tile)
+    assert (tmp_path / f"w{world}_{tile}_{split}.bin").read_bytes() == ref
+
+
+def test_frame_split_partitions_frames():
+    from flac_raster.tiles import calculate_tiles, frame_split, frames_of
+
+    tiles = calculate_tiles(10980, 10980, 1024)
+    F = sum(frames_of(t) for t in tiles)
+    for world in (1, 2, 3, 8):
+        parts = frame_split(tiles, world)
+        assert max(sum(n for _, _, n in p) for p in parts) - min(sum(n for _, _, n in p) for p in parts) <= 1
+        seen = {}
+        for p in parts:
+            for i, f0, n in p:
+                seen.setdefault(i, []).append((f0, n))
+        assert sorted(seen) == list(range(len(tiles)))
+        for i, rs in seen.items():  # every tile's frames exactly once, in order
+            rs.sort()
+            assert rs[0][0] == 0 and all(a + n == b for (a, n), (b, _) in zip(rs, rs[1:]))
+            assert rs[-1][0] + rs[-1][1] == frames_of(tiles[i])
+        assert sum(n for p in parts for _, _, n in p) == F
 
 
 def test_distributed_ranks_read_own_windows(tmp_path):
@@ -96,7 +121,7 @@ def test_distributed_ranks_read_own_windows(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), True), nprocs=2, join=True)
     ref = assemble_streaming(tiles, oracle_encode_tiles(r, tiles, 5), r.shape, r.dtype,
                              Affine(30.0, 0, 1000.0, 0, -30.0, 9000.0), "EPSG:3857", 64)
-    assert (tmp_path / "w2f.bin").read_bytes() == ref
+    assert (tmp_path / "w2f_64_frames.bin").read_bytes() == ref
 
 
 def test_shards_partition_tiles():

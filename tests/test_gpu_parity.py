@@ -321,6 +321,16 @@ def test_wave_kernel_incompressible_start(level):
     check_windows(r, [(0, 0, r.shape[1], 4096)], level, 16)
 
 
+@pytest.mark.parametrize("amp", [2000, 9000, 15000, 24000])
+def test_wave_kernel_large_rice_parameters(require_wave, amp):
+    """Noisy rasters whose kept LPC residuals still fit 16 bits but need Rice parameters up to 15-16: the packed
+    u16 shift-and-dot2 sums of the exact pass (shift counts capped, pairs weighted 0 past 15) against the oracle."""
+    rng = np.random.default_rng(amp)
+    base = synth_window(4, 23, 2, 128, 512).astype(np.int64)
+    r = np.clip(base // 4 + rng.integers(-amp, amp + 1, size=base.shape), 0, 65535).astype(np.uint16)
+    check_windows(r, [(0, 0, 128, 512), (0, 0, 64, 256)], 5, 16)
+
+
 def test_wave_kernel_constant_and_two_valued(require_wave):
     """Constant frames (CONSTANT subframes), two-valued frames and their mix in one stream."""
     base = synth_window(3, 11, 1, 64, 192)[0].astype(np.int64)

@@ -373,3 +373,34 @@ def test_frame_scan_forms_equal(monkeypatch, items):
     monkeypatch.setenv("FRA_SCAN_ITEMS", items)
     infos, got = N.encode_windows(r, wins, level=5, norm=16)
     assert got == ref
+
+
+@pytest.mark.parametrize("kind,dtype,level,norm", [(4, np.uint16, 5, 16), (5, np.float32, 8, 24)])
+def test_ranged_plan_frames_equal_stream_slices(kind, dtype, level, norm):
+    """fra_plan_create_ranged (the (tile, frame range) work items of the multi-GPU split): each window's
+    frames [f0, f0 + n) equal that slice of the whole-stream encode -- same normalisation (whole window),
+    same frame numbers -- including ranges that start mid-stream and end at the partial last frame."""
+    r = synth_window(kind, 13, 3, 1500, 1300).astype(dtype)
+    wins = calculate_tiles(1500, 1300, 512)
+    ctx = N.default_context(0)
+    full = N.Plan(ctx, None, False, r.dtype, 3, (1500 * 1300, 1300, 1), wins, level, 4096, norm)
+    try:
+        cap, _ = full.capacity()
+        out = np.empty(cap, np.uint8)
+        full.encode_host(r, out)
+        fi, _ = full.result()
+        offs = full.frame_offsets(sum(i.nframes for i in fi))
+    finally:
+        full.close()
+    nfr = [i.nframes for i in fi]
+    ranges = [((k * 7) % n, -1 if k % 3 == 0 else max(1, n // 3)) for k, n in enumerate(nfr)]
+    ri, rf = N.encode_windows_buffer(r, wins, level, 4096, norm, frame_ranges=ranges)
+    base = 0
+    for k, ((f0, n), info) in enumerate(zip(ranges, ri)):
+        n = nfr[k] - f0 if n < 0 else min(n, nfr[k] - f0)
+        g0 = base + f0
+        exp = bytes(out[offs[g0]:offs[g0 + n]])
+        assert bytes(rf[info.offset:info.offset + info.frame_bytes]) == exp, f"window {k} range {(f0, n)}"
+        assert info.nframes == n and info.sample_rate == fi[k].sample_rate
+        assert (info.data_min, info.data_max) == (fi[k].data_min, fi[k].data_max)
+        base += nfr[k]
