@@ -52,6 +52,10 @@ CONFIGS = {
     "c5": dict(kind=5, bands=8, H=32768, W=32768, dtype=np.float32, tile=512, level=8, norm=24,
                workload="C5 multispectral 32768x32768x8 float32 (normalize->int32, 32-bps), --streaming "
                         "--tile-size 512, -c 8"),
+    # profiling / A/B subset of C5 (a quarter of the scene, the same tiles, level and per-subframe work); never the
+    # bench line's workload
+    "c5q": dict(kind=5, bands=8, H=16384, W=16384, dtype=np.float32, tile=512, level=8, norm=24,
+                workload="C5 quarter (16384x16384x8 float32, tiles 512, -c 8): profiling subset"),
 }
 SEED = 20260227
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level parameters)

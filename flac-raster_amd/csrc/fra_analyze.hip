@@ -392,7 +392,7 @@ constexpr int kWaves16 = 6;  // waves per SIMD of the 16-bit lag <= 8 instance (
 template <bool B32, int MAXLAG>
 __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16)) k_analyze(JobArgs a, int src) {
   int g_ = a.frame_base + (int)blockIdx.x, c_ = (int)blockIdx.y;
-  if (!B32 && MAXLAG == 8 && a.part) {
+  if (a.part && ((!B32 && MAXLAG == 8) || (B32 && MAXLAG == 12))) {
     const int e = __builtin_amdgcn_readfirstlane(a.part[blockIdx.x]);
     g_ = e >> 3;
     c_ = e & 7;
@@ -1362,19 +1362,21 @@ namespace fra {
 #endif
 
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s);
+hipError_t launch_analyze_w32(int src, int level, const JobArgs& a, int cw, hipStream_t s);
 
 // wave: 16-bit plans whose full frames k_analyze_w takes (fra_api.hip wave_path): k_analyze_w over the launch's
 // frames, k_analyze over `part` (the launch's npart partial subframes, frame * 8 + channel), both complete
 // k_analyze over a list of partial subframes (frame * 8 + channel) on stream s (the pipelined execute runs it
 // on the norm stream right after the norm stage, a whole execute ahead of the frame scan that needs it)
-hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, int npart, int max_part_blocks,
-                               hipStream_t s) {
+hipError_t launch_analyze_part(int src, bool b32, const JobArgs& a, const int32_t* part, int npart,
+                               int max_part_blocks, hipStream_t s) {
   if (npart <= 0) return hipSuccess;
   JobArgs wa = a;
   wa.part = part;
   wa.npart = npart;
   (void)max_part_blocks;
-  k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, s>>>(wa, src);  // one workgroup per entry
+  if (b32) k_analyze<true, 12><<<(unsigned)npart, kThreads, 0, s>>>(wa, src);  // one workgroup per entry
+  else k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, s>>>(wa, src);
   return hipGetLastError();
 }
 
@@ -1387,14 +1389,15 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-  if (wave && !b32 && ml == 8) {
+  if (wave && ((!b32 && ml == 8) || (b32 && !ms && ml == 12))) {
     const int cw = ms ? 2 : a.cmax;
     hipError_t e = hipSuccess;
     auto partial = [&](hipStream_t ps) {
       JobArgs wa = a;
       wa.part = part;
       wa.npart = npart;
-      k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
+      if (b32) k_analyze<true, 12><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
+      else k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);
     };
     const bool fork = npart > 0 && side;
     if (fork) {
@@ -1403,7 +1406,8 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
       partial(side);
       if ((e = hipEventRecord(ev_join, side)) != hipSuccess) return e;
     }
-    if ((e = launch_analyze_w(src, a.level, a, cw, s)) != hipSuccess) return e;
+    if ((e = b32 ? launch_analyze_w32(src, a.level, a, cw, s) : launch_analyze_w(src, a.level, a, cw, s)) != hipSuccess)
+      return e;
     if (fork && (e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return e;
     if (npart > 0 && !side) partial(s);
     if (ms) {

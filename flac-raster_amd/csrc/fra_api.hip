@@ -33,7 +33,7 @@ hipError_t launch_norm_finalize(const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_norm_lut(int src, const JobArgs& a, int nstreams, hipStream_t s);
 hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStream_t s, bool wave, const int32_t* part,
                           int npart, int max_part_blocks, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join);
-hipError_t launch_analyze_part(int src, const JobArgs& a, const int32_t* part, int npart, int max_part_blocks,
+hipError_t launch_analyze_part(int src, bool b32, const JobArgs& a, const int32_t* part, int npart, int max_part_blocks,
                                hipStream_t s);
 int frame_scan_blocks(int nframes);
 hipError_t launch_frame_scan(const JobArgs& a, unsigned long long* gbase, int grp, int last, int add_base,
@@ -650,8 +650,10 @@ static int plan_build(fra_plan* p) {
       HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
       p->aux.push_back(st);
     }
-    if (!p->b32 && j.blocksize == kMaxBlock && j.level >= 3 && j.level <= 6 && j.norm != 0 &&
-        elem_size(j.dtype) <= 2 && j.dtype != FRA_F64) {  // plans k_analyze_w may take (wave_path)
+    if (j.blocksize == kMaxBlock && ((!p->b32 && j.level >= 3 && j.level <= 6 && j.norm != 0 &&
+                                      elem_size(j.dtype) <= 2 && j.dtype != FRA_F64) ||
+                                     (p->b32 && j.level >= 7 && j.norm == 24 && j.dtype == FRA_F32 &&
+                                      j.channels == p->cmax))) {  // plans k_analyze_w / k_analyze_w32 may take (wave_path)
       // the partial subframes (frame * 8 + channel, ascending): k_analyze's share of a wave-path launch
       p->h_part.clear();
       for (int g = 0; g < nfr; g++) {
@@ -911,8 +913,15 @@ static void collect_times(fra_plan* p) {
 // k_analyze as a list); FRA_ANALYZE_WG=1 keeps every frame on the workgroup kernel (tests compare both)
 static bool wave_path(const fra_plan* p) {
   const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
-  return !wg && p->wave_ok && !p->b32 && p->args.lut && p->args.vec8 && p->args.off32 && p->job.blocksize == kMaxBlock &&
-         p->job.level >= 3 && p->job.level <= 6;
+  if (wg || !p->wave_ok || !p->args.vec8 || !p->args.off32 || p->job.blocksize != kMaxBlock) return false;
+  if (p->b32) {  // k_analyze_w32 (r05, opt-in FRA_W32=1): float32 rasters normalised to 24 bits, levels 7-8.
+    // Bytes identical to k_analyze<true, 12>, but measured slower (C5 quarter 28.5 against 22.8 ms of analysis,
+    // profiles/r05_ab_w32_c5q.txt): at 16 KiB of LDS per wave only 2 waves per SIMD run, each re-reads and
+    // re-converts its samples per model (the workgroup kernel holds one chunk per thread across all models)
+    const bool w32 = getenv("FRA_W32") && atoi(getenv("FRA_W32")) == 1;
+    return w32 && p->job.norm == 24 && p->job.dtype == FRA_F32 && p->job.level >= 7 && p->job.level <= 8;
+  }
+  return p->args.lut && p->job.level >= 3 && p->job.level <= 6;  // k_analyze_w
 }
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
 // global offsets after the previous group's (event ordered), assembly.  ev_* null = serial.
@@ -963,7 +972,7 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     HIPCHK(hipEventRecord(ev_norm, norm_st));
     HIPCHK(hipStreamWaitEvent(st, ev_norm, 0));
     if (ev_part) {
-      HIPCHK(launch_analyze_part(p->src, ga, part, npart, 8 * p->ncu, norm_st));
+      HIPCHK(launch_analyze_part(p->src, p->b32, ga, part, npart, 8 * p->ncu, norm_st));
       HIPCHK(hipEventRecord(ev_part, norm_st));
     }
   }

@@ -14,6 +14,6 @@ for CTRS in "SQ_WAVES SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FMA_
             "SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- \
-    python $GRAFT_REPO_ROOT/tools/diag_phases.py ${LIB:--} > $OUT/p$i.log 2>&1 || echo "pass $i failed" >> $OUT/fail.log
+    python $GRAFT_REPO_ROOT/tools/diag_phases.py ${LIB:--} ${CFG:-c4} > $OUT/p$i.log 2>&1 || echo "pass $i failed" >> $OUT/fail.log
 done
 echo done
