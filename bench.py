@@ -373,9 +373,9 @@ def main():
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="time rank R's LPT share of the scene for an N-GPU strong-scaling run, on this one GPU "
                          "(projection of the multi-GPU step; DESIGN.md section 7)")
-    ap.add_argument("--split", default="frames", choices=["frames", "lpt"],
+    ap.add_argument("--split", default="frames", choices=["frames", "strided", "lpt"],
                     help="strong scaling: (tile, frame range) work items of equal frame count per rank (default; "
-                         "fra_plan_create_ranged) or whole tiles by LPT")
+                         "fra_plan_create_ranged), the same over the tiles in strided order, or whole tiles by LPT")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
     ap.add_argument("--no-trace", action="store_true", help="skip the in-run rocprofv3 kernel-trace pass")
@@ -439,9 +439,9 @@ def main():
     nparts = shard_of[1] if shard_of is not None else (1 if weak else world)
     if shard_of is not None:
         rank = shard_of[0]
-    if args.split == "frames" or nparts == 1:
+    if args.split in ("frames", "strided") or nparts == 1:
         from flac_raster.tiles import frame_split
-        items = frame_split(wins, nparts)[rank if nparts > 1 else 0]
+        items = frame_split(wins, nparts, stride=nparts if args.split == "strided" else 1)[rank if nparts > 1 else 0]
     else:
         owner = lpt_shard(wins, nparts)
         items = [(i, 0, -(-(wins[i][2] * wins[i][3]) // 4096)) for i in range(len(wins)) if owner[i] == rank]
@@ -507,8 +507,11 @@ def main():
                                        "pack": round(per_launch_ms[3], 4)},
               "fixed_ms_per_step": round(T / args.steps * 1e3 - per_launch_ms[1], 4),
               "projected_job_mpix_s": round(H * W / (T / args.steps) / 1e6, 2),
-              "note": "projected, unmeasured on hardware: one GPU runs this rank's LPT tile share of the scene; "
-                      "the N-GPU step is the slowest rank's step (LPT imbalance <= 1.022 on C4)"}
+              "split": args.split, "frames": sum(n for _, _, n in items),
+              "note": "projected, unmeasured on hardware: one GPU runs this rank's share of the scene ("
+                      + {"frames": "equal frame ranges", "strided": "equal frame ranges over strided tiles",
+                         "lpt": "LPT tiles"}[args.split]
+                      + "); the N-GPU step is the slowest rank's step"}
         print(json.dumps(sh), flush=True)
         plan.close()
         ctx.free(dev_raster)

@@ -168,9 +168,10 @@ def rank_items(tiles: Sequence[Tuple[int, int, int, int]], world: int, rank: int
                split: str = "frames") -> List[Tuple[int, int, int]]:
     """This rank's work items (tile index, first frame, frame count): ``split="frames"`` -- equal frame
     counts per rank (``frame_split``: whole tiles plus at most a partial tile at each end, SURVEY.md 8(e)'s
-    (tile, frame-range) items); ``"lpt"`` -- whole tiles by LPT on pixel count."""
-    if split == "frames":
-        return frame_split(tiles, world)[rank]
+    (tile, frame-range) items); ``"strided"`` -- the same over the tiles in strided order (tile index mod
+    world first: every rank samples the whole scene); ``"lpt"`` -- whole tiles by LPT on pixel count."""
+    if split in ("frames", "strided"):
+        return frame_split(tiles, world, stride=world if split == "strided" else 1)[rank]
     return [(i, 0, frames_of(tiles[i])) for i in shard(tiles, world, rank)]
 
 

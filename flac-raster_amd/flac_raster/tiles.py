@@ -56,17 +56,22 @@ def frames_of(tile: Tuple[int, int, int, int], blocksize: int = 4096) -> int:
 
 
 def frame_split(tiles: Sequence[Tuple[int, int, int, int]], parts: int,
-                blocksize: int = 4096) -> List[List[Tuple[int, int, int]]]:
+                blocksize: int = 4096, stride: int = 1) -> List[List[Tuple[int, int, int]]]:
     """Work items of equal size for ``parts`` ranks ((tile, frame range) items): the frames
     of all tiles in tile order, cut into ``parts`` contiguous runs of equal frame count; part k gets a list
     of (tile index, first frame, frame count) -- whole tiles, plus at most a partial tile at each end.  The
-    frames of one tile, concatenated over the parts in order, are that tile's stream."""
+    frames of one tile, concatenated over the parts in order, are that tile's stream.
+
+    ``stride`` > 1 visits the tiles as i = 0, s, 2s, ..., then 1, 1 + s, ... (tile index mod s first), so each
+    part's run samples the whole scene instead of one band of it: content that varies across the scene (a
+    no-data corner, water, cloud) spreads over the parts, while the frame counts stay equal."""
     counts = [frames_of(t, blocksize) for t in tiles]
     total = sum(counts)
     cuts = [total * k // parts for k in range(parts + 1)]
     out: List[List[Tuple[int, int, int]]] = [[] for _ in range(parts)]
     base = 0
-    for i, n in enumerate(counts):
+    for i in sorted(range(len(tiles)), key=lambda j: (j % max(1, stride), j)):
+        n = counts[i]
         for k in range(parts):
             a, b = max(base, cuts[k]), min(base + n, cuts[k + 1])
             if b > a:

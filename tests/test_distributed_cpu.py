@@ -59,7 +59,7 @@ def _worker(rank, world, port, out_dir, from_file=False, tile=64, split="frames"
 
 
 @pytest.mark.parametrize("world,tile,split", [(2, 64, "frames"), (3, 64, "lpt"), (3, 128, "frames"),
-                                              (2, 160, "frames")])
+                                              (2, 160, "frames"), (3, 64, "strided")])
 def test_distributed_container_identical(tmp_path, world, tile, split):
     """World 2/3, whole-tile LPT items and (tile, frame range) items: with tiles of 4-7 frames the equal
     frame-count split cuts tiles between ranks, whose frame slices the writer joins back into streams."""
@@ -79,13 +79,16 @@ def test_distributed_container_identical(tmp_path, world, tile, split):
     assert (tmp_path / f"w{world}_{tile}_{split}.bin").read_bytes() == ref
 
 
-def test_frame_split_partitions_frames():
+@pytest.mark.parametrize("strided", [False, True])
+def test_frame_split_partitions_frames(strided):
     from flac_raster.tiles import calculate_tiles, frame_split, frames_of
 
     tiles = calculate_tiles(10980, 10980, 1024)
     F = sum(frames_of(t) for t in tiles)
     for world in (1, 2, 3, 8):
-        parts = frame_split(tiles, world)
+        parts = frame_split(tiles, world, stride=world if strided else 1)
+        if strided and world == 8:  # every part's run spans the scene (tiles of every row band)
+            assert all(max(i for i, _, _ in p) - min(i for i, _, _ in p) > len(tiles) // 2 for p in parts)
         assert max(sum(n for _, _, n in p) for p in parts) - min(sum(n for _, _, n in p) for p in parts) <= 1
         seen = {}
         for p in parts:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Same-box A/B of the pipelined step: ab_step.py <config> <lib.so|-> [NAME=VALUE ...]
 
-Environment assignments are applied before the plan is created (FRA_CHUNK_MB, FRA_ANALYZE_WG, ...).
+Environment assignments are applied before the plan is created (FRA_CHUNK_MB, FRA_ANALYZE_WG, ...);
+SHARD=R/N encodes only rank R's frame-split share of the scene (bench.py --shard).
 Prints the serial per-kernel times (timing mode, 5 executes) and the pipelined step time (median of
 5 runs of 20 back-to-back executes, wall clock around a sync), plus the output size as a bytes check."""
 import os
@@ -32,7 +33,15 @@ dt = np.dtype(cfg["dtype"])
 dev = ctx.alloc(B * H * W * dt.itemsize)
 ctx.synth(cfg["kind"], bench.SEED, B, H, W, dev)
 wins = bench.tiles(H, W, cfg["tile"])
-plan = N.Plan(ctx, dev, True, dt, B, (H * W, W, 1), wins, cfg["level"], 4096, cfg["norm"])
+ranges = None
+shard = os.environ.get("SHARD")  # R/N: rank R's frame-split share (bench.py --shard)
+if shard:
+    from flac_raster.tiles import frame_split
+    sr, sn = (int(x) for x in shard.split("/"))
+    items = frame_split(wins, sn)[sr]
+    wins = [wins[i] for i, _, _ in items]
+    ranges = [(f0, n) for _, f0, n in items]
+plan = N.Plan(ctx, dev, True, dt, B, (H * W, W, 1), wins, cfg["level"], 4096, cfg["norm"], frame_ranges=ranges)
 plan.execute(); plan.sync()
 plan.enable_timing(True)
 for _ in range(5):
