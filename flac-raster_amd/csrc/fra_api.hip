@@ -2,8 +2,8 @@
 //
 // A plan owns every device buffer a job needs (raster copy if host-resident, stream/frame tables,
 // window tables, subframe descriptors, frame sizes/offsets, output, scan workspace), so that
-// fra_plan_execute() only enqueues kernels on the context's stream: no allocation, no host sync
-// (graph-capturable).  Per-job launch sequence (fra_kernels.hip):
+// fra_plan_execute() only enqueues kernels and events: no allocation, no host sync; the frame scan's
+// ticket / epoch state lives on the device, not in launch arguments.  Per-job launch sequence (fra_kernels.hip):
 //   k_norm_init, k_minmax, k_norm_finalize  (skipped when norm == 0)
 //   k_analyze  [frames x channels]
 //   k_frame_scan (frame sizes + decoupled look-back scan; k_group_offsets after a previous group)
@@ -16,11 +16,15 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <ctime>
+#include <deque>
 #include <map>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/flac_raster_amd.h"
@@ -140,6 +144,8 @@ struct fra_plan {
   std::vector<hipEvent_t> hev;          // per band: rows copied, frames assembled (+ end offset mirrored)
   hipEvent_t hev_start = nullptr;
   unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
+  uint8_t* h_stage = nullptr;  // page-locked staging of the D2H workers (pageable outputs), h_stage_n pieces
+  int h_stage_n = 0;
   unsigned long long* d_gbase_mirror = nullptr;  // its device address
   // cross-execute pipelining (FRA_PIPE, default on when a second buffer set fits in a third of the free
   // device memory, single frame group): execute k analyses into buffer set k % 2 on the plan's stream
@@ -370,6 +376,7 @@ void fra_plan_destroy(fra_plan* p) {
     if (e) (void)hipEventDestroy(e);
   if (p->hev_start) (void)hipEventDestroy(p->hev_start);
   if (p->h_gbase) (void)hipHostFree(p->h_gbase);
+  if (p->h_stage) (void)hipHostFree(p->h_stage);
   for (auto& e : p->gev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : p->ev)
@@ -1248,6 +1255,84 @@ static int copy_rows_ring_h2d(fra_plan* p, const RingIn& rg, int64_t r0, int64_t
   return FRA_OK;
 }
 
+// page-locked (hipHostMalloc'd or registered) host memory: an async copy to it returns at once
+static bool host_pinned(const void* ptr) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+// encode_host's D2H copies into a pageable output, on threads of their own (`out` null: off, the caller copies
+// itself).  The runtime's own copy into pageable memory stages through one pinned buffer and copies out on the
+// calling thread, page faults of a lazily committed buffer included: about 17 GB/s, so C5's 22.4 GB of frames
+// outlasted the 34 GB raster's H2D by 0.6 s (profiles/r05_ring_timeline.txt).  Here each of n threads owns a
+// 64 MiB piece of page-locked staging: DMA the piece into it at the link rate, then copy it out on that thread,
+// so the copy-outs and their page faults run n-wide beside the DMA.  push() takes a byte range whose frames are
+// complete on the device.
+struct D2HWorker {
+  static constexpr uint64_t kPiece = 64ull << 20;
+  D2HWorker(int device, uint8_t* out, const uint8_t* dev, uint8_t* stage, int n) : out_(out), dev_(dev) {
+    if (!out_) return;
+    for (int i = 0; i < n; i++) th_.emplace_back([this, device, stage, i]() { run(device, stage + (uint64_t)i * kPiece); });
+  }
+  ~D2HWorker() { finish(); }
+  bool on() const { return out_ != nullptr; }
+  void push(uint64_t a, uint64_t b) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (uint64_t x = a; x < b; x += kPiece) q_.emplace_back(x, std::min(b, x + kPiece));
+    }
+    cv_.notify_all();
+  }
+  // wait for every pushed copy; false if one failed (error())
+  bool finish() {
+    if (!th_.empty()) {
+      { std::lock_guard<std::mutex> lk(mu_); end_ = true; }
+      cv_.notify_all();
+      for (auto& t : th_) t.join();
+      th_.clear();
+    }
+    return err_.empty();
+  }
+  const std::string& error() const { return err_; }
+
+ private:
+  void run(int device, uint8_t* stage) {
+    (void)hipSetDevice(device);
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    for (;;) {
+      std::pair<uint64_t, uint64_t> r;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return !q_.empty() || end_; });
+        if (q_.empty()) break;
+        r = q_.front();
+        q_.pop_front();
+      }
+      if (e != hipSuccess) continue;  // drain the queue after a failure
+      const size_t n = (size_t)(r.second - r.first);
+      e = hipMemcpyAsync(stage, dev_ + r.first, n, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e == hipSuccess) memcpy(out_ + r.first, stage, n);
+    }
+    if (st) (void)hipStreamDestroy(st);
+    if (e != hipSuccess) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (err_.empty()) err_ = hipGetErrorString(e);
+    }
+  }
+  uint8_t* out_;
+  const uint8_t* dev_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<uint64_t, uint64_t>> q_;
+  bool end_ = false;
+  std::string err_;  // read after the joins
+};
 static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
                        uint64_t* total_bytes, const volatile int64_t* rows_ready, const RingIn* ring = nullptr);
 int fra_plan_encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, uint64_t capacity,
@@ -1357,20 +1442,35 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
   uint64_t beg = 0;
   int issued = 0;  // bands whose D2H has been enqueued
   bool over = false;
+  // a pageable output (the ring path's lazily committed frames): a D2H into it returns only once the runtime has
+  // staged the whole copy, which would hold this loop -- and with it the next band's H2D and the producer's ring
+  // rows -- for every band's frames; those copies go to worker threads instead
+  const bool out_pageable = capacity > 0 && !host_pinned(host_out);
+  if (out_pageable && !p->h_stage) {  // FRA_D2H_THREADS (default 4) pieces of staging, kept by the plan
+    const char* e = getenv("FRA_D2H_THREADS");
+    p->h_stage_n = std::min(std::max(e ? atoi(e) : 4, 1), 16);
+    HIPCHK(hipHostMalloc((void**)&p->h_stage, D2HWorker::kPiece * p->h_stage_n, hipHostMallocPortable));
+  }
+  D2HWorker dw(p->ctx->device, out_pageable ? host_out : nullptr, p->d_out, p->h_stage, p->h_stage_n);
   auto enqueue_d2h = [&](int b) -> int {
     const uint64_t end = p->h_gbase[b + 1];
     if (end > capacity) over = true;
     if (!over && end > beg) {
-      HIPCHK(hipStreamWaitEvent(p->d2h, p->hev[2 * b + 1], 0));
-      HIPCHK(hipMemcpyAsync(host_out + beg, p->d_out + beg, (size_t)(end - beg), hipMemcpyDeviceToHost, p->d2h));
+      if (dw.on()) {
+        dw.push(beg, end);
+      } else {
+        HIPCHK(hipStreamWaitEvent(p->d2h, p->hev[2 * b + 1], 0));
+        HIPCHK(hipMemcpyAsync(host_out + beg, p->d_out + beg, (size_t)(end - beg), hipMemcpyDeviceToHost, p->d2h));
+      }
     }
     beg = end;
     return FRA_OK;
   };
-  // an error after work was enqueued (a failed producer, a HIP error): drain the three streams before
-  // returning, so no copy still reads the caller's buffers
+  // an error after work was enqueued (a failed producer, a HIP error): drain the three streams (and the D2H
+  // worker) before returning, so no copy still reads or writes the caller's buffers
   auto drained = [&](int code) -> int {
     std::string keep = g_err;
+    dw.finish();
     (void)hipStreamSynchronize(p->h2d);
     (void)hipStreamSynchronize(s);
     (void)hipStreamSynchronize(p->d2h);
@@ -1402,6 +1502,7 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
     HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
     if ((rc = enqueue_d2h(issued++))) return drained(rc);
   }
+  if (!dw.finish()) return drained(set_err(FRA_E_HIP, "frames D2H: %s", dw.error().c_str()));
   HIPCHK(hipStreamSynchronize(p->d2h));
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipStreamSynchronize(p->h2d));
