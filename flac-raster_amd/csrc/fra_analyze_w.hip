@@ -255,18 +255,18 @@ __device__ __forceinline__ int32_t wnorm(uint32_t r, const WNorm& q) {
   return (int32_t)u;  // (in [-32767, 32767]: the clamps of norm_sample never act on the tile's own values)
 }
 template <typename T>
-__device__ __forceinline__ void wload_lut(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+__device__ __forceinline__ void wload_lut(const void* base, const WaveDev& wd, int c,
                                           const int32_t* lut, uint32_t* sw, int lane, uint32_t& orv, int32_t& vmin,
                                           int32_t& vmax, bool stamp, const WNorm& wn) {
   constexpr int V = 8 / (int)sizeof(T);
   constexpr int NV = kMaxBlock / 64 / V;
   constexpr uint32_t step = 64 * V;
   using VT = VecT<T, V>;
-  const uint32_t w = (uint32_t)st.width;
-  const char* b0 = (const char*)((const T*)base + st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride);
-  const uint32_t rsb = (uint32_t)st.row_stride * (uint32_t)sizeof(T);
+  const uint32_t w = wd.width;
+  const char* b0 = (const char*)((const T*)base + wd.off0 + (int64_t)c * wd.band_stride);
+  const uint32_t rsb = wd.row_stride * (uint32_t)sizeof(T);
   const uint32_t qs = step / w, rs = step - qs * w, rstep = qs * rsb;  // uniform
-  uint32_t col = (uint32_t)fr.col0 + (uint32_t)lane * V;
+  uint32_t col = wd.col0 + (uint32_t)lane * V;
   uint32_t roff = 0;
   if (col >= w) {
     const uint32_t q = col / w;
@@ -376,13 +376,12 @@ k_analyze_w(JobArgs a, int src) {
   FRA_WSTAMP(0)
   const int g = a.frame_base + (int)blockIdx.x;
   const int c = (int)blockIdx.y;
-  const FrameDev fr = a.frames[g];
-  const StreamDev st = a.streams[fr.stream];
-  if (c >= (st.ms ? 2 : st.channels)) return;
+  const WaveDev wd = a.wave[g];
+  if (c >= wd.nch) return;
   FRA_WSTAMP_WAIT(10)
-  if (fr.n != kMaxBlock) return;  // partial last frames: k_analyze, over the plan's list of them
+  if (wd.n != kMaxBlock) return;  // partial last frames: k_analyze, over the plan's list of them
   constexpr int n = kMaxBlock;
-  const int bps = st.bps;
+  const int bps = wd.bps;
   const LevelCfg cfg = level_cfg(a.level);
   SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
   uint32_t* const slot = a.tmp + ((size_t)g * a.cmax + c) * a.tmp_stride;
@@ -398,18 +397,18 @@ k_analyze_w(JobArgs a, int src) {
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   // (the lambdas capture these locals, not the kernel arguments: taking the arguments' address costs registers)
   const void* const raster = a.raster;
-  const int32_t* const lut = a.lut + (int64_t)fr.stream * a.lut_stride;
+  const int32_t* const lut = a.lut + (int64_t)wd.stream * a.lut_stride;
   WNorm wn{};
   if (FRA_W_ARITH) {
-    const NormParams np = norm_params(st, a.norm[fr.stream]);
+    const NormParams np = norm_params(a.streams[wd.stream], a.norm[wd.stream]);
     wn.two_mn = -2.0 * np.mn;
     wn.range = np.range;
     wn.rcp = np.rcp;
     wn.flip = src == ST_I16 ? 0x8000u : (src == ST_I8 ? 0x80u : 0u);
   }
   auto load_samples = [&](uint32_t& ov, int32_t& mn, int32_t& mx, bool first) {
-    if (src == ST_U8 || src == ST_I8) wload_lut<uint8_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first, wn);  // uniform
-    else wload_lut<uint16_t>(raster, st, fr, c, lut, sw, lane, ov, mn, mx, first, wn);
+    if (src == ST_U8 || src == ST_I8) wload_lut<uint8_t>(raster, wd, c, lut, sw, lane, ov, mn, mx, first, wn);  // uniform
+    else wload_lut<uint16_t>(raster, wd, c, lut, sw, lane, ov, mn, mx, first, wn);
   };
   load_samples(orv, vmin, vmax, true);
   orv = wave_or32(orv);
@@ -536,10 +535,10 @@ k_analyze_w(JobArgs a, int src) {
 #pragma unroll
       for (int l = 0; l < NL; l++) acl[l] = 0.0;
       for (int wi = 0; wi < nwin; wi++) {
-        const int32_t* wr = a.wrange + 2 * ((size_t)fr.win * a.nwin + wi);
-        const int32_t* wp = a.wplat + 2 * ((size_t)fr.win * a.nwin + wi);
+        const int32_t* wr = a.wrange + 2 * ((size_t)wd.win * a.nwin + wi);
+        const int32_t* wp = a.wplat + 2 * ((size_t)wd.win * a.nwin + wi);
         const int lo = wr[0], hi = wr[1], plo = wp[0], phi = wp[1];
-        const float* win = a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize;
+        const float* win = a.win + ((size_t)wd.win * a.nwin + wi) * a.blocksize;
         double s01[N16], s[N16];
 #pragma unroll
         for (int k = 0; k < N16; k++) { s01[k] = 0.0; s[k] = 0.0; }
@@ -1146,6 +1145,7 @@ hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStr
   const dim3 grid((unsigned)a.frame_count, (unsigned)cw);
   const LevelCfg cfg = level_cfg(level);
   if (cfg.nsub == 0 || cfg.max_lpc > 8) return hipErrorInvalidValue;  // levels 3-6 only
+  if (!a.wave) return hipErrorInvalidValue;  // the plan's per-frame descriptors (wave-path plans)
   switch (cfg.max_porder) {
     case 4: k_analyze_w<8, 4><<<grid, 64, 0, s>>>(a, src); break;
     case 5: k_analyze_w<8, 5><<<grid, 64, 0, s>>>(a, src); break;

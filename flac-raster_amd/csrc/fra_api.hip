@@ -74,6 +74,12 @@ static int set_err(int code, const char* fmt, ...) {
 struct fra_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // encode_host's D2H workers for pageable outputs: page-locked staging (stage_n pieces of 64 MiB) and one stream
+  // per worker, kept across plans (the file path builds a plan per call); one encode at a time holds them
+  std::mutex stage_mu;
+  uint8_t* stage = nullptr;
+  int stage_n = 0;
+  std::vector<hipStream_t> stage_st;
 };
 
 struct fra_plan {
@@ -106,6 +112,7 @@ struct fra_plan {
   // a launch over frames [f0, f1) passes the entries in [8 f0, 8 f1))
   std::vector<int32_t> h_part;
   int32_t* d_part = nullptr;
+  WaveDev* d_wave = nullptr;  // k_analyze_w's per-frame descriptors (JobArgs::wave)
   bool wave_ok = false;
   hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
   hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
@@ -144,8 +151,6 @@ struct fra_plan {
   std::vector<hipEvent_t> hev;          // per band: rows copied, frames assembled (+ end offset mirrored)
   hipEvent_t hev_start = nullptr;
   unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
-  uint8_t* h_stage = nullptr;  // page-locked staging of the D2H workers (pageable outputs), h_stage_n pieces
-  int h_stage_n = 0;
   unsigned long long* d_gbase_mirror = nullptr;  // its device address
   // cross-execute pipelining (FRA_PIPE, default on when a second buffer set fits in a third of the free
   // device memory, single frame group): execute k analyses into buffer set k % 2 on the plan's stream
@@ -313,6 +318,8 @@ void fra_ctx_destroy(fra_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (auto st : c->stage_st) (void)hipStreamDestroy(st);
+  if (c->stage) (void)hipHostFree(c->stage);
   delete c;
 }
 
@@ -327,6 +334,7 @@ void fra_plan_destroy(fra_plan* p) {
   (void)hipFree(p->d_wrange);
   (void)hipFree(p->d_wplat);
   (void)hipFree(p->d_part);
+  (void)hipFree(p->d_wave);
   if (p->pside) (void)hipStreamDestroy(p->pside);
   if (p->ev_pfork) (void)hipEventDestroy(p->ev_pfork);
   if (p->ev_pjoin) (void)hipEventDestroy(p->ev_pjoin);
@@ -376,7 +384,6 @@ void fra_plan_destroy(fra_plan* p) {
     if (e) (void)hipEventDestroy(e);
   if (p->hev_start) (void)hipEventDestroy(p->hev_start);
   if (p->h_gbase) (void)hipHostFree(p->h_gbase);
-  if (p->h_stage) (void)hipHostFree(p->h_stage);
   for (auto& e : p->gev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : p->ev)
@@ -673,6 +680,26 @@ static int plan_build(fra_plan* p) {
       if (!p->h_part.empty())
         HIPCHK(hipMemcpy(p->d_part, p->h_part.data(), sizeof(int32_t) * p->h_part.size(), hipMemcpyHostToDevice));
       p->wave_ok = true;
+      {  // k_analyze_w's per-frame descriptors (WaveDev)
+        std::vector<WaveDev> wv(std::max(1, nfr));
+        for (int g = 0; g < nfr; g++) {
+          const FrameDev& fr = p->frames[g];
+          const StreamDev& st = p->streams[fr.stream];
+          WaveDev& w = wv[g];
+          w.off0 = st.base_off + (int64_t)fr.row0 * st.row_stride;
+          w.band_stride = st.band_stride;
+          w.row_stride = (uint32_t)st.row_stride;
+          w.width = (uint32_t)st.width;
+          w.col0 = (uint32_t)fr.col0;
+          w.stream = fr.stream;
+          w.n = fr.n;
+          w.win = fr.win;
+          w.bps = st.bps;
+          w.nch = st.ms ? 2 : st.channels;
+        }
+        HIPCHK(hipMalloc(&p->d_wave, sizeof(WaveDev) * wv.size()));
+        HIPCHK(hipMemcpy(p->d_wave, wv.data(), sizeof(WaveDev) * wv.size(), hipMemcpyHostToDevice));
+      }
       if (!p->h_part.empty()) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -703,6 +730,7 @@ static int plan_build(fra_plan* p) {
   JobArgs& a = p->args;
   a.streams = p->d_streams;
   a.frames = p->d_frames;
+  a.wave = p->d_wave;
   a.norm = p->d_norm;
   a.win = p->d_win;
   a.wrange = p->d_wrange;
@@ -1273,9 +1301,11 @@ static bool host_pinned(const void* ptr) {
 // complete on the device.
 struct D2HWorker {
   static constexpr uint64_t kPiece = 64ull << 20;
-  D2HWorker(int device, uint8_t* out, const uint8_t* dev, uint8_t* stage, int n) : out_(out), dev_(dev) {
+  D2HWorker(int device, uint8_t* out, const uint8_t* dev, uint8_t* stage, const std::vector<hipStream_t>& st)
+      : out_(out), dev_(dev) {
     if (!out_) return;
-    for (int i = 0; i < n; i++) th_.emplace_back([this, device, stage, i]() { run(device, stage + (uint64_t)i * kPiece); });
+    for (size_t i = 0; i < st.size(); i++)
+      th_.emplace_back([this, device, stage, i, s = st[i]]() { run(device, stage + (uint64_t)i * kPiece, s); });
   }
   ~D2HWorker() { finish(); }
   bool on() const { return out_ != nullptr; }
@@ -1299,10 +1329,8 @@ struct D2HWorker {
   const std::string& error() const { return err_; }
 
  private:
-  void run(int device, uint8_t* stage) {
-    (void)hipSetDevice(device);
-    hipStream_t st = nullptr;
-    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  void run(int device, uint8_t* stage, hipStream_t st) {
+    hipError_t e = hipSetDevice(device);
     for (;;) {
       std::pair<uint64_t, uint64_t> r;
       {
@@ -1318,7 +1346,6 @@ struct D2HWorker {
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (e == hipSuccess) memcpy(out_ + r.first, stage, n);
     }
-    if (st) (void)hipStreamDestroy(st);
     if (e != hipSuccess) {
       std::lock_guard<std::mutex> lk(mu_);
       if (err_.empty()) err_ = hipGetErrorString(e);
@@ -1445,13 +1472,23 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
   // a pageable output (the ring path's lazily committed frames): a D2H into it returns only once the runtime has
   // staged the whole copy, which would hold this loop -- and with it the next band's H2D and the producer's ring
   // rows -- for every band's frames; those copies go to worker threads instead
-  const bool out_pageable = capacity > 0 && !host_pinned(host_out);
-  if (out_pageable && !p->h_stage) {  // FRA_D2H_THREADS (default 4) pieces of staging, kept by the plan
+  // (the context's staging and streams: FRA_D2H_THREADS workers, default 4; held for this call -- a concurrent
+  // encode on the same context copies through the runtime instead)
+  fra_ctx* cx = p->ctx;
+  std::unique_lock<std::mutex> stage_lk(cx->stage_mu, std::defer_lock);
+  const bool out_pageable = capacity > 0 && !host_pinned(host_out) && stage_lk.try_lock();
+  if (out_pageable && !cx->stage) {
     const char* e = getenv("FRA_D2H_THREADS");
-    p->h_stage_n = std::min(std::max(e ? atoi(e) : 4, 1), 16);
-    HIPCHK(hipHostMalloc((void**)&p->h_stage, D2HWorker::kPiece * p->h_stage_n, hipHostMallocPortable));
+    const int n = std::min(std::max(e ? atoi(e) : 4, 1), 16);
+    HIPCHK(hipHostMalloc((void**)&cx->stage, D2HWorker::kPiece * n, hipHostMallocPortable));
+    cx->stage_n = n;
+    for (int i = 0; i < n; i++) {
+      hipStream_t st = nullptr;
+      HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      cx->stage_st.push_back(st);
+    }
   }
-  D2HWorker dw(p->ctx->device, out_pageable ? host_out : nullptr, p->d_out, p->h_stage, p->h_stage_n);
+  D2HWorker dw(cx->device, out_pageable ? host_out : nullptr, p->d_out, cx->stage, cx->stage_st);
   auto enqueue_d2h = [&](int b) -> int {
     const uint64_t end = p->h_gbase[b + 1];
     if (end > capacity) over = true;

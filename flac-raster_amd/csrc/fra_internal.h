@@ -157,6 +157,21 @@ struct FrameDev {
   int32_t row0, col0;  // window-relative pixel position of sample 0
 };
 
+// k_analyze_w's per-frame metadata (wave-path plans, built at plan creation): everything its load phase needs in
+// ONE scalar load, instead of FrameDev -> StreamDev (two dependent round trips before the first raw row)
+struct WaveDev {
+  int64_t off0;         // element offset of band 0, the frame's first row (StreamDev base_off + row0 * row_stride)
+  int64_t band_stride;  // elements between channels
+  uint32_t row_stride;  // elements between rows
+  uint32_t width;       // window width (col_stride 1)
+  uint32_t col0;        // window-relative column of sample 0
+  int32_t stream;       // stream index (normalisation table row)
+  int32_t n;            // block size of the frame
+  int32_t win;          // window-table index
+  int32_t bps;          // FLAC bits per sample
+  int32_t nch;          // channels the wave kernel analyses (mid-side: L and R)
+};
+
 struct NormDev {       // per stream, filled on device
   unsigned long long mnkey, mxkey;  // ordered-key min/max (NaN excluded)
   double mn, mx, range;             // normalize_to_audio parameters (normalization.py:148-159)
@@ -221,6 +236,7 @@ struct JobArgs {
   int32_t npart;           //   subframes of the launch's frames, npart entries (null: the normal grid)
   uint32_t* err;           // plan error word (checked at every sync): bit 0 frame-scan ticket desync, bit 1 a
                            //   frame outside its output / slot bounds (not written)
+  const WaveDev* wave;     // [nframes_total] (wave-path plans; else null)
 };
 
 }  // namespace fra
