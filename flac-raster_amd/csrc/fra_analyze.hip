@@ -409,16 +409,17 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   // single-wave phases do not always land on the same SIMD; data layout (sample ranges, per-wave partials,
   // the encoder's scan) keeps the physical wave index wv
   const int rw = (wv + rot) & 3;
-  const FrameDev fr = a.frames[g];
-  const StreamDev st = a.streams[fr.stream];
+  // the frame's analysis descriptor first: the load phase takes its addresses, block size and stream from it,
+  // so the raw loads wait for one scalar load instead of FrameDev -> StreamDev
+  const WaveDev wd = a.wave[g];
   // mid-side streams (FRA-1 3.1b): virtual channels 0 L, 1 R, 2 M, 3 S; L and R are analysed by the
   // 16-bit instance, M and S (bps + 1 bits) by the 32-bit one, whose grid rows 0-1 are channels 2-3
-  const int c = cy + ((B32 && st.ms) ? 2 : 0);
+  const int c = cy + ((B32 && wd.ms) ? 2 : 0);
   FRA_STAMP(0)
-  if (c >= (st.ms ? (B32 ? 4 : 2) : st.channels)) return;
-  const int n = fr.n;
-  const int bps = st.bps + ((st.ms && c == 3) ? 1 : 0);
-  const int msmode = (st.ms && c >= 2) ? c - 1 : 0;
+  if (c >= (wd.ms ? (B32 ? 4 : 2) : wd.channels)) return;
+  const int n = wd.n;
+  const int bps = wd.bps + ((wd.ms && c == 3) ? 1 : 0);
+  const int msmode = (wd.ms && c >= 2) ? c - 1 : 0;
   const LevelCfg cfg = level_cfg(a.level);
   SfDesc* d = &a.sf[(size_t)g * a.cmax + c];
 #ifdef FRA_DIAG_STOP
@@ -439,17 +440,17 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   uint32_t orv = 0;
   int32_t vmin = INT32_MAX, vmax = INT32_MIN;
   {
-    const NormParams np = norm_params(st, a.norm[fr.stream]);
-    const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)fr.stream * a.lut_stride : nullptr;
-    FRA_LOAD_STAMP(11, (int)np.mn + st.width + fr.n)
+    const NormParams np = norm_params(wd.norm, a.norm[wd.stream]);
+    const int32_t* lut = (a.lut && np.mode) ? a.lut + (int64_t)wd.stream * a.lut_stride : nullptr;
+    FRA_LOAD_STAMP(11, (int)np.mn + (int)wd.width + wd.n)
     bool done = false;
     if constexpr (!B32) {
       if (lut && a.vec8 && a.off32 && n == kMaxBlock) {
-        done = load_lut_full(src, a.raster, st, fr, c, lut, S.smp, orv, vmin, vmax);
+        done = load_lut_full(src, a.raster, wd, c, lut, S.smp, orv, vmin, vmax);
         pf_ok = done && pf_allowed;  // (the prefetch target is found by dispatch order)
       }
     }
-    if (!done) load_channel(src, a.vec8 != 0, a.raster, st, fr, c, np, lut, S.smp, orv, vmin, vmax, msmode);
+    if (!done) load_channel(src, a.vec8 != 0, a.raster, wd, a.streams + wd.stream, a.frames + g, c, np, lut, S.smp, orv, vmin, vmax, msmode);
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
@@ -559,7 +560,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   // samples + lookahead [1024 wv, 1024 wv + 1024 + MAXLAG) miss it would only sum exact products of
   // zeros, i.e. every chunk partial is +0.0 -- it skips the window and stores those zeros directly
   auto wave_active = [&](const int wi) -> bool {
-    const int32_t* r = a.wrange + 2 * ((size_t)fr.win * a.nwin + wi);
+    const int32_t* r = a.wrange + 2 * ((size_t)wd.win * a.nwin + wi);
     const int lo = __builtin_amdgcn_readfirstlane(r[0]), hi = __builtin_amdgcn_readfirstlane(r[1]);
     const int w0 = wv * 64 * kChunk;
     return lo < w0 + 64 * kChunk + MAXLAG && hi > w0;
@@ -581,7 +582,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
         // exact-1.0 coefficients here, unlike k_analyze_w: its SGPR pressure cost more than the loads it saved,
         // C5 117.0 -> 115.2 ms without it, profiles/r04_ab_plateau_k_analyze_c5.txt)
         float wcoef[kChunk + MAXLAG];
-        load_window<MAXLAG>(a.win + ((size_t)fr.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
+        load_window<MAXLAG>(a.win + ((size_t)wd.win * a.nwin + wi) * a.blocksize, i0, n, wcoef);
         float wf[kChunk + MAXLAG];
         {
           int32_t y[kChunk + 8];

@@ -112,7 +112,7 @@ struct fra_plan {
   // a launch over frames [f0, f1) passes the entries in [8 f0, 8 f1))
   std::vector<int32_t> h_part;
   int32_t* d_part = nullptr;
-  WaveDev* d_wave = nullptr;  // k_analyze_w's per-frame descriptors (JobArgs::wave)
+  WaveDev* d_wave = nullptr;  // per-frame analysis descriptors (JobArgs::wave)
   bool wave_ok = false;
   hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
   hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
@@ -622,6 +622,29 @@ static int plan_build(fra_plan* p) {
   if (!p->streams.empty())
     HIPCHK(hipMemcpy(p->d_streams, p->streams.data(), sizeof(StreamDev) * p->streams.size(), hipMemcpyHostToDevice));
   if (nfr) HIPCHK(hipMemcpy(p->d_frames, p->frames.data(), sizeof(FrameDev) * nfr, hipMemcpyHostToDevice));
+  {  // per-frame analysis descriptors (WaveDev: the load phase's metadata in one scalar load)
+    std::vector<WaveDev> wv(std::max(1, nfr));
+    for (int g = 0; g < nfr; g++) {
+      const FrameDev& fr = p->frames[g];
+      const StreamDev& st = p->streams[fr.stream];
+      WaveDev& w = wv[g];
+      w.off0 = st.base_off + (int64_t)fr.row0 * st.row_stride;
+      w.band_stride = st.band_stride;
+      w.row_stride = (uint32_t)st.row_stride;
+      w.width = (uint32_t)st.width;
+      w.col0 = (uint32_t)fr.col0;
+      w.stream = fr.stream;
+      w.n = fr.n;
+      w.win = fr.win;
+      w.bps = st.bps;
+      w.nch = st.ms ? 2 : st.channels;
+      w.channels = st.channels;
+      w.ms = st.ms;
+      w.norm = st.norm;
+    }
+    HIPCHK(hipMalloc(&p->d_wave, sizeof(WaveDev) * wv.size()));
+    HIPCHK(hipMemcpy(p->d_wave, wv.data(), sizeof(WaveDev) * wv.size(), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemset(p->d_norm, 0, sizeof(NormDev) * std::max<size_t>(1, p->streams.size())));
   // frame groups: FRA_GROUPS (default 1: measured no gain on C4) contiguous window runs of about equal frame count;
   // one group for small plans, where launch latency dominates
@@ -680,26 +703,6 @@ static int plan_build(fra_plan* p) {
       if (!p->h_part.empty())
         HIPCHK(hipMemcpy(p->d_part, p->h_part.data(), sizeof(int32_t) * p->h_part.size(), hipMemcpyHostToDevice));
       p->wave_ok = true;
-      {  // k_analyze_w's per-frame descriptors (WaveDev)
-        std::vector<WaveDev> wv(std::max(1, nfr));
-        for (int g = 0; g < nfr; g++) {
-          const FrameDev& fr = p->frames[g];
-          const StreamDev& st = p->streams[fr.stream];
-          WaveDev& w = wv[g];
-          w.off0 = st.base_off + (int64_t)fr.row0 * st.row_stride;
-          w.band_stride = st.band_stride;
-          w.row_stride = (uint32_t)st.row_stride;
-          w.width = (uint32_t)st.width;
-          w.col0 = (uint32_t)fr.col0;
-          w.stream = fr.stream;
-          w.n = fr.n;
-          w.win = fr.win;
-          w.bps = st.bps;
-          w.nch = st.ms ? 2 : st.channels;
-        }
-        HIPCHK(hipMalloc(&p->d_wave, sizeof(WaveDev) * wv.size()));
-        HIPCHK(hipMemcpy(p->d_wave, wv.data(), sizeof(WaveDev) * wv.size(), hipMemcpyHostToDevice));
-      }
       if (!p->h_part.empty()) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));

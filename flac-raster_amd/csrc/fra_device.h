@@ -54,11 +54,11 @@ struct NormParams {
   bool to16;
   int mode;  // 0 raw ints, else normalise
 };
-__device__ __forceinline__ NormParams norm_params(const StreamDev& st, const NormDev& nd) {
+__device__ __forceinline__ NormParams norm_params(int norm, const NormDev& nd) {
   NormParams p;
-  p.mode = st.norm;
-  p.to16 = st.norm == 16;
-  p.scale = st.norm == 16 ? 32767.0 : 8388607.0;
+  p.mode = norm;
+  p.to16 = norm == 16;
+  p.scale = norm == 16 ? 32767.0 : 8388607.0;
   double mn, mx;
   if (nd.mnkey == ~0ull) {  // no non-NaN value: nanmin/nanmax -> NaN
     mn = __longlong_as_double(0x7FF8000000000000ll);
@@ -72,6 +72,7 @@ __device__ __forceinline__ NormParams norm_params(const StreamDev& st, const Nor
   p.rcp = 1.0 / p.range;
   return p;
 }
+__device__ __forceinline__ NormParams norm_params(const StreamDev& st, const NormDev& nd) { return norm_params(st.norm, nd); }
 // t/range for the integer dtypes by Markstein's reciprocal refinement: bit-identical to the IEEE
 // quotient for every t = 2*(x-mn) in [0, 2R], R integer (exhaustively verified for R < 2^16 by
 // tools/verify_markstein.c; theorem-backed for 32-bit integers: no under/overflow is possible).
@@ -131,25 +132,26 @@ struct alignas(sizeof(T) * V) VecT {
 // host checked that no vector straddles a row and all are aligned: JobArgs::vec8), thread t owns
 // vectors t + 256k; otherwise one element per lane, samples t + 256k.  Returns per-thread OR/min/max.
 template <int SRC, bool VEC, typename SmpT>
-__device__ __forceinline__ void load_raw_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
-                                           typename RawType<SRC>::T (&raw)[kMaxBlock / kThreads]) {
+__device__ __forceinline__ void load_raw_t(const void* base, const WaveDev& wd, const StreamDev* stp, const FrameDev* frp,
+                                           int c, typename RawType<SRC>::T (&raw)[kMaxBlock / kThreads]) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
   constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
   const T* src = (const T*)base;
-  const int n = fr.n, w = st.width, t = threadIdx.x;
-  if constexpr (VEC) {
+  const int n = wd.n, w = (int)wd.width, t = threadIdx.x;
+  if constexpr (VEC) {  // (addresses from the frame's WaveDev only: no StreamDev round trip before the loads)
     using VT = VecT<T, V>;
-    int col = fr.col0 + t * V, row = fr.row0;
+    int col = (int)wd.col0 + t * V, row = 0;
     if (col >= w) {
       const int q = (int)((unsigned)col / (unsigned)w);
       row += q;
       col -= q * w;
     }
-    int64_t e = st.base_off + (int64_t)c * st.band_stride + (int64_t)row * st.row_stride + col;
+    const int64_t rs = (int64_t)wd.row_stride;
+    int64_t e = wd.off0 + (int64_t)c * wd.band_stride + (int64_t)row * rs + col;
     const int step = kThreads * V;
-    const int64_t wrap = st.row_stride - (int64_t)w;
-    const int64_t e_first = st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride + fr.col0;
+    const int64_t wrap = rs - (int64_t)w;
+    const int64_t e_first = wd.off0 + (int64_t)c * wd.band_stride + (int64_t)wd.col0;
 #pragma unroll
     for (int kv = 0; kv < K / V; kv++) {
       const VT x = *(const VT*)(src + (((t + kv * kThreads) * V < n) ? e : e_first));
@@ -166,7 +168,9 @@ __device__ __forceinline__ void load_raw_t(const void* base, const StreamDev& st
         }
       }
     }
-  } else {
+  } else {  // (element strides: StreamDev / FrameDev read here only, not kept live through the kernel)
+  const StreamDev& st = *stp;
+  const FrameDev& fr = *frp;
   int col = fr.col0 + t, row = fr.row0;
   if (col >= w) {
     const int q = (int)((unsigned)col / (unsigned)w);
@@ -200,27 +204,27 @@ __device__ __forceinline__ void load_raw_t(const void* base, const StreamDev& st
 // (32-bit instance only; |l|, |r| < 2^15 since mid-side streams are 16-bps).  Channel 0 is parked in this
 // thread's own smp slots, then combined with channel 1.
 template <int SRC, bool VEC>
-__device__ __forceinline__ void load_mid_side_t(const void* base, const StreamDev& st, const FrameDev& fr,
+__device__ __forceinline__ void load_mid_side_t(const void* base, const WaveDev& wd, const StreamDev* st, const FrameDev* fr,
                                              const NormParams& np, const int32_t* lut, int32_t* smp, uint32_t& orv,
                                              int32_t& vmin, int32_t& vmax, int msmode) {
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
   constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
   constexpr bool kLutType = SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16;
-  const int n = fr.n, t = threadIdx.x;
+  const int n = wd.n, t = threadIdx.x;
   auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
   auto audio = [&](T r) -> int32_t {
     if (kLutType && lut) return lut[lut_index<SRC>(r)];
     return np.mode == 0 ? (int32_t)r : norm_sample<SRC>((double)r, np);
   };
   T raw[K];
-  load_raw_t<SRC, VEC, int32_t>(base, st, fr, 0, raw);
+  load_raw_t<SRC, VEC, int32_t>(base, wd, st, fr, 0, raw);
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int i = sidx_of(k);
     if (i < n) smp[sidx(smp, i)] = audio(raw[k]);
   }
-  load_raw_t<SRC, VEC, int32_t>(base, st, fr, 1, raw);
+  load_raw_t<SRC, VEC, int32_t>(base, wd, st, fr, 1, raw);
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int i = sidx_of(k);
@@ -238,22 +242,22 @@ __device__ __forceinline__ void load_mid_side_t(const void* base, const StreamDe
 // ints when norm == 0): all of a thread's loads are issued before any is consumed.  Returns
 // per-thread OR/min/max.  msmode != 0: the mid-side virtual channels (32-bit instance).
 template <int SRC, bool VEC, typename SmpT>
-__device__ __forceinline__ void load_channel_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+__device__ __forceinline__ void load_channel_t(const void* base, const WaveDev& wd, const StreamDev* st, const FrameDev* fr, int c,
                                                const NormParams& np, const int32_t* lut, SmpT* smp, uint32_t& orv,
                                                int32_t& vmin, int32_t& vmax, int msmode) {
   if constexpr (std::is_same<SmpT, int32_t>::value) {
     if (msmode) {
-      load_mid_side_t<SRC, VEC>(base, st, fr, np, lut, smp, orv, vmin, vmax, msmode);
+      load_mid_side_t<SRC, VEC>(base, wd, st, fr, np, lut, smp, orv, vmin, vmax, msmode);
       return;
     }
   }
   using T = typename RawType<SRC>::T;
   constexpr int K = kMaxBlock / kThreads;
   constexpr int V = VEC ? 8 / (int)sizeof(T) : 1;
-  const int n = fr.n, t = threadIdx.x;
+  const int n = wd.n, t = threadIdx.x;
   auto sidx_of = [&](int k) { return VEC ? (t + (k / V) * kThreads) * V + (k % V) : t + k * kThreads; };
   T raw[K];
-  load_raw_t<SRC, VEC, SmpT>(base, st, fr, c, raw);
+  load_raw_t<SRC, VEC, SmpT>(base, wd, st, fr, c, raw);
   FRA_LOAD_STAMP(12, (int)raw[0] + (int)raw[K - 1])
   if constexpr (SRC == ST_U8 || SRC == ST_I8 || SRC == ST_U16 || SRC == ST_I16) {
     if (lut) {  // <= 16-bit integers: the normalised sample of value v is lut[lut_index(v)] (k_norm_lut)
@@ -294,7 +298,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const StreamDev
 // and stored 4 at a time (ds_write_b64: a thread's 4 or 8 consecutive samples lie in one 16-sample chunk),
 // OR / min / max on the packed pairs (v_pk_min_i16 / v_pk_max_i16).  No per-sample bounds (n == 4096).
 template <int SRC>
-__device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDev& st, const FrameDev& fr, int c,
+__device__ __forceinline__ void load_lut_full_t(const void* base, const WaveDev& wd, int c,
                                                 const int32_t* lut, int16_t* smp, uint32_t& orv, int32_t& vmin,
                                                 int32_t& vmax) {
   using T = typename RawType<SRC>::T;
@@ -302,10 +306,10 @@ __device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDe
   constexpr int NV = kMaxBlock / kThreads / V;          // vectors per thread
   constexpr int step = kThreads * V;
   using VT = VecT<T, V>;
-  const int w = st.width, t = threadIdx.x;
-  const char* b0 = (const char*)((const T*)base + st.base_off + (int64_t)c * st.band_stride + (int64_t)fr.row0 * st.row_stride);
-  const uint32_t rsb = (uint32_t)st.row_stride * (uint32_t)sizeof(T);
-  int col = fr.col0 + t * V;
+  const int w = (int)wd.width, t = threadIdx.x;
+  const char* b0 = (const char*)((const T*)base + wd.off0 + (int64_t)c * wd.band_stride);
+  const uint32_t rsb = wd.row_stride * (uint32_t)sizeof(T);
+  int col = (int)wd.col0 + t * V;
   uint32_t roff = 0;
   if (col >= w) {
     const int q = (int)((unsigned)col / (unsigned)w);
@@ -354,43 +358,43 @@ __device__ __forceinline__ void load_lut_full_t(const void* base, const StreamDe
   vmin = min(vmin, min((int32_t)pmin.x, (int32_t)pmin.y));
   vmax = max(vmax, max((int32_t)pmax.x, (int32_t)pmax.y));
 }
-__device__ __forceinline__ bool load_lut_full(int src, const void* base, const StreamDev& st, const FrameDev& fr, int c,
+__device__ __forceinline__ bool load_lut_full(int src, const void* base, const WaveDev& wd, int c,
                                               const int32_t* lut, int16_t* smp, uint32_t& orv, int32_t& vmin,
                                               int32_t& vmax) {
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_lut_full_t<ST_U8>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
-    case ST_I8: load_lut_full_t<ST_I8>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
-    case ST_U16: load_lut_full_t<ST_U16>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
-    case ST_I16: load_lut_full_t<ST_I16>(base, st, fr, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_U8: load_lut_full_t<ST_U8>(base, wd, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_I8: load_lut_full_t<ST_I8>(base, wd, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_U16: load_lut_full_t<ST_U16>(base, wd, c, lut, smp, orv, vmin, vmax); return true;
+    case ST_I16: load_lut_full_t<ST_I16>(base, wd, c, lut, smp, orv, vmin, vmax); return true;
     default: return false;
   }
 }
 
 template <typename SmpT>
-__device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const StreamDev& st, const FrameDev& fr,
+__device__ __forceinline__ void load_channel(int src, bool vec8, const void* base, const WaveDev& wd, const StreamDev* st, const FrameDev* fr,
                                              int c, const NormParams& np, const int32_t* lut, SmpT* smp,
                                              uint32_t& orv, int32_t& vmin, int32_t& vmax, int msmode) {
   if (vec8) {
     switch (src) {  // wave-uniform dispatch; f64 never takes the vector path
-      case ST_U8: load_channel_t<ST_U8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_I8: load_channel_t<ST_I8, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_U16: load_channel_t<ST_U16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_I16: load_channel_t<ST_I16, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_U32: load_channel_t<ST_U32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_I32: load_channel_t<ST_I32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
-      case ST_F32: load_channel_t<ST_F32, true, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_U8: load_channel_t<ST_U8, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I8: load_channel_t<ST_I8, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_U16: load_channel_t<ST_U16, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I16: load_channel_t<ST_I16, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_U32: load_channel_t<ST_U32, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_I32: load_channel_t<ST_I32, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
+      case ST_F32: load_channel_t<ST_F32, true, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); return;
       default: break;
     }
   }
   switch (src) {  // wave-uniform dispatch
-    case ST_U8: load_channel_t<ST_U8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_I8: load_channel_t<ST_I8, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_U16: load_channel_t<ST_U16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_I16: load_channel_t<ST_I16, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_U32: load_channel_t<ST_U32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_I32: load_channel_t<ST_I32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    case ST_F32: load_channel_t<ST_F32, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
-    default: load_channel_t<ST_F64, false, SmpT>(base, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_U8: load_channel_t<ST_U8, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I8: load_channel_t<ST_I8, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_U16: load_channel_t<ST_U16, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I16: load_channel_t<ST_I16, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_U32: load_channel_t<ST_U32, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_I32: load_channel_t<ST_I32, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    case ST_F32: load_channel_t<ST_F32, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
+    default: load_channel_t<ST_F64, false, SmpT>(base, wd, st, fr, c, np, lut, smp, orv, vmin, vmax, msmode); break;
   }
 }
 

@@ -157,8 +157,8 @@ struct FrameDev {
   int32_t row0, col0;  // window-relative pixel position of sample 0
 };
 
-// k_analyze_w's per-frame metadata (wave-path plans, built at plan creation): everything its load phase needs in
-// ONE scalar load, instead of FrameDev -> StreamDev (two dependent round trips before the first raw row)
+// per-frame analysis metadata (built at plan creation): everything the load phase of k_analyze_w / k_analyze needs
+// in ONE scalar load, instead of FrameDev -> StreamDev (two dependent round trips before the first raw row)
 struct WaveDev {
   int64_t off0;         // element offset of band 0, the frame's first row (StreamDev base_off + row0 * row_stride)
   int64_t band_stride;  // elements between channels
@@ -170,6 +170,9 @@ struct WaveDev {
   int32_t win;          // window-table index
   int32_t bps;          // FLAC bits per sample
   int32_t nch;          // channels the wave kernel analyses (mid-side: L and R)
+  int32_t channels;     // StreamDev::channels
+  int32_t ms;           // StreamDev::ms
+  int32_t norm;         // StreamDev::norm
 };
 
 struct NormDev {       // per stream, filled on device
@@ -236,7 +239,7 @@ struct JobArgs {
   int32_t npart;           //   subframes of the launch's frames, npart entries (null: the normal grid)
   uint32_t* err;           // plan error word (checked at every sync): bit 0 frame-scan ticket desync, bit 1 a
                            //   frame outside its output / slot bounds (not written)
-  const WaveDev* wave;     // [nframes_total] (wave-path plans; else null)
+  const WaveDev* wave;     // [nframes_total]
 };
 
 }  // namespace fra
