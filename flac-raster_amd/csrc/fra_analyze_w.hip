@@ -360,9 +360,15 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
 // sums and the partition search are straight code instead of uniform branches on a runtime order -- branches
 // that also split the blocks the scheduler could otherwise overlap the ds_bpermute round trips in
 template <int MAXLAG, int PCAP>
-// occupancy target: 8 KiB of LDS lets 20 waves share a CU; <= 96 VGPRs make it 5 per SIMD
+// occupancy target: 4 waves per SIMD (r05).  8 KiB of LDS would let 20 waves share a CU and <= 96 VGPRs make it 5 per
+// SIMD, but at 4 (97 VGPRs here) the CU keeps 32 KiB of LDS and a wave slot per SIMD for the norm stage and the
+// assembly of the neighbouring executes, which then run beside the analysis instead of in its gaps: C4 step
+// 1.535-1.539 -> 1.516-1.525 ms, C3 1.062-1.068 -> 1.043-1.045, C4 8-way share 0.243-0.247 -> 0.234-0.239 same box
+// (profiles/r05_ab_four_waves.txt; r04 measured this cap neutral on its kernel).  The attribute lets the compiler
+// take more than 96 VGPRs, which it does for levels 5-6 (97); the level 3-4 instance stays at 95 and 5 per SIMD.
+// FRA_W_WAVES=5 builds the old target
 #ifndef FRA_W_WAVES
-#define FRA_W_WAVES 5
+#define FRA_W_WAVES 4
 #endif
 #ifndef FRA_W_WAVES_MAX
 #define FRA_W_WAVES_MAX 8
