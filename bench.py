@@ -270,14 +270,31 @@ def inrun_pmc(args, kernel):
     return res
 
 
-def codegen_stats(kernel):
-    """code bytes, VGPRs, SGPRs and spill counts of ``kernel`` in the loaded library's gfx950 code object
-    (tools/codeobj_stats.py), so codegen regressions show up in the bench record."""
+def analysis_kernel(cfg, dt):
+    """(label, mangled-name prefix) of the analysis kernel a plan of this config launches: k_analyze_w for full
+    frames of <= 16-bit normalised rasters at levels 3-6 (fra_api.hip wave_path; the partial-frame list goes to
+    k_analyze beside it), else the k_analyze instance of the sample width and the level's lag."""
+    lvl = cfg["level"]
+    if (np.dtype(dt).itemsize <= 2 and cfg["norm"] != 0 and 3 <= lvl <= 6
+            and os.environ.get("FRA_ANALYZE_WG", "0") == "0"):
+        pcap = {3: 4, 4: 4, 5: 5, 6: 6}[lvl]
+        return ("k_analyze_w (+ k_analyze over the partial-frame list, same phase)",
+                f"_ZN3fra11k_analyze_wILi8ELi{pcap}E")
+    b32 = 1 if cfg["norm"] == 24 or np.dtype(dt).itemsize > 2 else 0
+    lag = 12 if lvl >= 7 else (8 if lvl >= 3 else 0)
+    return "k_analyze", f"_ZN3fra9k_analyzeILb{b32}ELi{lag}E"
+
+
+def codegen_stats(kernel, prefix=None):
+    """code bytes, VGPRs, SGPRs and spill counts of ``kernel`` (the instance whose mangled name starts with
+    ``prefix`` when given) in the loaded library's gfx950 code object (tools/codeobj_stats.py), so codegen
+    regressions show up in the bench record."""
     try:
         sys.path.insert(0, str(ROOT / "tools"))
         import codeobj_stats
-        rows = [r for r in codeobj_stats.stats(str(N_LIB_PATH()), kernel) if r["kernel"].split("I")[0].endswith(kernel)
-                or f"{len(kernel)}{kernel}" in r["kernel"]]
+        rows = [r for r in codeobj_stats.stats(str(N_LIB_PATH()), kernel)
+                if (r["kernel"].startswith(prefix) if prefix else
+                    (r["kernel"].split("I")[0].endswith(kernel) or f"{len(kernel)}{kernel}" in r["kernel"]))]
         if not rows:
             return None
         r = max(rows, key=lambda r: r["code_bytes"])
@@ -598,11 +615,14 @@ def main():
         if pm is None:
             pm = committed_profile(args, cfg, dom_name)
         # the kernel the analysis phase's HIP events time: k_analyze_w (+ the partial-frame k_analyze list beside
-        # it) on 16-bit LUT plans at levels 3-6, k_analyze otherwise (inrun_pmc names the group)
+        # it) on 16-bit LUT plans at levels 3-6, k_analyze otherwise -- from the config, so lines without in-run
+        # counters (N > 1) name it too
         dom_label = dom_name
-        if pm.get("kernels"):
-            dom_label = "k_analyze_w (+ k_analyze over the partial-frame list, same phase)"
-        codegen = codegen_stats("k_analyze_w" if pm.get("kernels") else dom_name)
+        codegen = codegen_stats(dom_name)
+        if dom_name == "k_analyze":
+            dom_label, prefix = analysis_kernel(cfg, dt)
+            codegen = codegen_stats(prefix.split("ILb")[0].split("ILi")[0].rsplit("fra", 1)[1].lstrip("0123456789"),
+                                    prefix)
         hbm_frac = achieved / HBM_PEAK_GBPS
         valu_frac = None
         if pm.get("valu_insts") and pm.get("busy_cycles_per_xcd"):
