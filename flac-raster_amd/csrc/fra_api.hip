@@ -904,6 +904,9 @@ static int plan_create(fra_ctx* ctx, const fra_job* job, const int32_t* franges,
     return set_err(FRA_E_INVALID, "norm == 0 (pre-normalised audio) needs int16 or int32 samples");
   if (job->nwindows < 0 || (job->nwindows > 0 && !job->windows)) return set_err(FRA_E_INVALID, "bad windows");
   if (job->first_frame < 0) return set_err(FRA_E_INVALID, "first_frame must be >= 0");
+  // (the analysis descriptors hold the row stride in 32 bits: WaveDev)
+  if (job->band_stride < 0 || job->row_stride < 0 || job->col_stride < 1 || job->row_stride > (int64_t)UINT32_MAX)
+    return set_err(FRA_E_INVALID, "strides must be >= 0 (col_stride >= 1) with row_stride < 2^32 elements");
   for (int w = 0; w < job->nwindows; w++) {
     const fra_window& wd = job->windows[w];
     if (wd.height < 0 || wd.width < 0 || wd.row_off < 0 || wd.col_off < 0 || (wd.height > 0) != (wd.width > 0))

@@ -404,3 +404,13 @@ def test_ranged_plan_frames_equal_stream_slices(kind, dtype, level, norm):
         assert info.nframes == n and info.sample_rate == fi[k].sample_rate
         assert (info.data_min, info.data_max) == (fi[k].data_min, fi[k].data_max)
         base += nfr[k]
+
+
+def test_plan_rejects_bad_strides():
+    """Strides are validated at plan creation (negative strides, col_stride < 1, row_stride >= 2^32 elements:
+    the per-frame analysis descriptors hold the row stride in 32 bits)."""
+    ctx = N.default_context(0)
+    wins = calculate_tiles(16, 16, 16)
+    for strides in [(256, 2 ** 32, 1), (256, -16, 1), (256, 16, 0), (-256, 16, 1)]:
+        with pytest.raises(N.NativeError, match="strides"):
+            N.Plan(ctx, None, False, np.uint16, 1, strides, wins, 5, 4096, 16)
