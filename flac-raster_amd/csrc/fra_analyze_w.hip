@@ -695,7 +695,12 @@ k_analyze_w(JobArgs a, int src) {
   // recomputing the predictor twice (fallback: the samples are loaded again)
   // windows with a usable model (lanes 24 + wi of mv with an order)
   const uint32_t okm = (uint32_t)(__ballot(lane >= 24 && lane < 24 + kWinW && (mv >> 8) != 0) >> 24);
-  const int keep_wi = okm ? 31 - __clz((int)okm) : -1;
+  // the window whose residuals are kept: the first usable one (FRA_W_KEEP=0; window 0, the whole-block tukey,
+  // is the likeliest winner) or the last (FRA_W_KEEP=1); its sum pass runs last, after the other windows' passes
+#ifndef FRA_W_KEEP
+#define FRA_W_KEEP 0
+#endif
+  const int keep_wi = okm ? (FRA_W_KEEP ? 31 - __clz((int)okm) : __builtin_ctz(okm)) : -1;
   bool kept_fit = false;
   uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
 #pragma unroll 1
@@ -707,7 +712,7 @@ k_analyze_w(JobArgs a, int src) {
       m = o = ci == 0 ? g1 : g2;
       psum = ci == 0 ? pf1 : pf2;
     } else {
-      const int wi = ci - 2;
+      const int wi = (ci - 2 + keep_wi + 1) % nlpc;  // the keep window last (nlpc >= 1 here)
       if (!((okm >> wi) & 1u)) continue;  // no order / not quantisable
       const uint32_t inf = (uint32_t)__builtin_amdgcn_readlane((int)mv, 24 + wi);
       o = (int)(inf >> 8);
