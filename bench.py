@@ -270,13 +270,12 @@ def inrun_pmc(args, kernel):
     return res
 
 
-def analysis_kernel(cfg, dt):
-    """(label, mangled-name prefix) of the analysis kernel a plan of this config launches: k_analyze_w for full
-    frames of <= 16-bit normalised rasters at levels 3-6 (fra_api.hip wave_path; the partial-frame list goes to
-    k_analyze beside it), else the k_analyze instance of the sample width and the level's lag."""
+def analysis_kernel(cfg, dt, wave):
+    """(label, mangled-name prefix) of the analysis kernel a plan of this config launches: k_analyze_w when the plan
+    reports FRA_PLAN_WAVE (``wave``: full frames one subframe per wave, the partial-frame list on k_analyze beside
+    it) for a <= 16-bit raster, else the k_analyze instance of the sample width and the level's lag."""
     lvl = cfg["level"]
-    if (np.dtype(dt).itemsize <= 2 and cfg["norm"] != 0 and 3 <= lvl <= 6
-            and os.environ.get("FRA_ANALYZE_WG", "0") == "0"):
+    if wave and np.dtype(dt).itemsize <= 2:
         pcap = {3: 4, 4: 4, 5: 5, 6: 6}[lvl]
         return ("k_analyze_w (+ k_analyze over the partial-frame list, same phase)",
                 f"_ZN3fra11k_analyze_wILi8ELi{pcap}E")
@@ -468,6 +467,7 @@ def main():
     ranges = None if full else [(f0, n) for _, f0, n in items]
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"],
                   frame_ranges=ranges)
+    wave_plan = bool(plan.flags() & 4)  # FRA_PLAN_WAVE: full frames on k_analyze_w
 
     if args.child:  # rocprofv3 child: the plan's launches only
         if args.child_serial:  # the roofline's mode: serial executes, each kernel alone on the device
@@ -620,7 +620,7 @@ def main():
         dom_label = dom_name
         codegen = codegen_stats(dom_name)
         if dom_name == "k_analyze":
-            dom_label, prefix = analysis_kernel(cfg, dt)
+            dom_label, prefix = analysis_kernel(cfg, dt, wave_plan)
             codegen = codegen_stats(prefix.split("ILb")[0].split("ILi")[0].rsplit("fra", 1)[1].lstrip("0123456789"),
                                     prefix)
         hbm_frac = achieved / HBM_PEAK_GBPS

@@ -1230,7 +1230,9 @@ int fra_plan_set_first_frame(fra_plan* p, int32_t first_frame) {
 
 int fra_plan_flags(fra_plan* p, int32_t* flags) {
   if (!p || !flags) return set_err(FRA_E_INVALID, "null argument");
-  *flags = p->pipe ? FRA_PLAN_PIPELINED : 0;
+  // (vector loads as an execute will decide them: the device raster's alignment, or hipMalloc's for host rasters)
+  p->args.vec8 = (p->ld_vec8 && (!p->d_raster || (uintptr_t)p->d_raster % 8 == 0)) ? 1 : 0;
+  *flags = (p->pipe ? FRA_PLAN_PIPELINED : 0) | (wave_path(p) ? FRA_PLAN_WAVE : 0);
   return FRA_OK;
 }
 

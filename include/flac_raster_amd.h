@@ -169,10 +169,13 @@ FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
 FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
 /* how the plan encodes (FRA_PLAN_*): PIPELINED = executes overlap (double-buffered subframe slots, the
- * next execute's normalisation stage and this one's assembly run beside k_analyze).  FRA_PLAN_DIRECT_WRITE
- * is never set (the direct-write path was measured slower than slots + k_assemble and removed in r03). */
+ * next execute's normalisation stage and this one's assembly run beside k_analyze); WAVE = full frames are
+ * analysed one subframe per wave (k_analyze_w, or k_analyze_w32 when enabled), the partial ones by k_analyze
+ * beside it; otherwise every subframe goes to the k_analyze workgroup kernel.  FRA_PLAN_DIRECT_WRITE is never
+ * set (the direct-write path was measured slower than slots + k_assemble and removed in r03). */
 #define FRA_PLAN_DIRECT_WRITE 1
 #define FRA_PLAN_PIPELINED 2
+#define FRA_PLAN_WAVE 4
 FRA_API int fra_plan_flags(fra_plan *plan, int32_t *flags);
 
 /* page-locked host memory (hipHostMalloc / hipHostRegister, portable across devices) */

@@ -414,3 +414,19 @@ def test_plan_rejects_bad_strides():
     for strides in [(256, 2 ** 32, 1), (256, -16, 1), (256, 16, 0), (-256, 16, 1)]:
         with pytest.raises(N.NativeError, match="strides"):
             N.Plan(ctx, None, False, np.uint16, 1, strides, wins, 5, 4096, 16)
+
+
+@pytest.mark.parametrize("dtype,level,norm,wave", [
+    (np.uint16, 5, 16, True), (np.int16, 6, 16, True), (np.uint8, 3, 16, True),   # k_analyze_w: levels 3-6
+    (np.uint16, 8, 16, False), (np.uint16, 2, 16, False),                         # lag 12 / no LPC: k_analyze
+    (np.float32, 8, 24, False), (np.int32, 5, 24, False),                         # 32-bps: k_analyze
+])
+def test_plan_reports_analysis_path(dtype, level, norm, wave):
+    """fra_plan_flags reports FRA_PLAN_WAVE exactly when full frames take the per-wave analysis kernel (bench.py
+    names the dominant kernel from it)."""
+    wins = calculate_tiles(512, 512, 256)
+    plan = N.Plan(N.default_context(0), None, False, np.dtype(dtype), 1, (512 * 512, 512, 1), wins, level, 4096, norm)
+    try:
+        assert bool(plan.flags() & 4) == wave
+    finally:
+        plan.close()
