@@ -430,3 +430,27 @@ def test_plan_reports_analysis_path(dtype, level, norm, wave):
         assert bool(plan.flags() & 4) == wave
     finally:
         plan.close()
+
+
+@pytest.mark.parametrize("threads", [1, 7])
+def test_encode_host_pageable_output_worker_counts(threads, monkeypatch):
+    """A pageable output is filled by the context's D2H workers through page-locked staging (FRA_D2H_THREADS,
+    read when a context first needs them): one worker and an odd count give the device path's bytes, into a
+    fresh (lazily committed) buffer and into one already written."""
+    monkeypatch.setenv("FRA_D2H_THREADS", str(threads))
+    r = synth_window(4, 5, 4, 3600, 3600)
+    wins = calculate_tiles(3600, 3600, 1024)
+    di, df = _device_path(r, wins, 5, 16)
+    ctx = N.Context(0)
+    plan = N.Plan(ctx, None, False, r.dtype, 4, (3600 * 3600, 3600, 1), wins, 5, 4096, 16)
+    try:
+        cap, nbands = plan.capacity()
+        assert nbands > 1
+        for _ in range(2):
+            out = np.empty(cap, np.uint8)
+            total = plan.encode_host(r, out)
+            assert bytes(out[:total]) == df
+        assert plan.encode_host(r, out) == total and bytes(out[:total]) == df  # pages already committed
+    finally:
+        plan.close()
+        ctx.close()
