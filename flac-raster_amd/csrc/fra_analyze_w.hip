@@ -326,16 +326,17 @@ __device__ __forceinline__ uint32_t lpc_abs16_w(const uint32_t (&D)[14], const i
   return acc;
 }
 
-// the same sum, plus the chunk's zig-zag residuals packed two per dword (u[2p] low, u[2p+1] high; exact
-// whenever every u < 2^16, which `um`, the OR of all u, tells)
+// the same sum, plus the chunk's zig-zag residuals packed two per dword (u[2p] low, u[2p+1] high: their low 16
+// bits) and bit 16 of each in `hb` (bit jj; r05): exact whenever every u < 2^17, which `um`, the OR of all u, tells
 template <int O>
 __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const int32_t* q, int sh, bool head,
-                                                 uint32_t (&pk)[kChunk / 2], uint32_t& um) {
+                                                 uint32_t (&pk)[kChunk / 2], uint32_t& um, uint32_t& hb) {
   constexpr int NP = (O + 1) / 2;
   fra_short2 Q[NP];
   q_pairs_rev<NP>(q, Q);
   uint32_t acc = 0;
   uint32_t u[kChunk];
+  hb = 0;
 #pragma unroll
   for (int jj = 0; jj < kChunk; jj++) {
     const int32_t r = sample_at(D, 12 + jj) - (pred_raw<NP>(D, 12 + jj, Q) >> sh);
@@ -347,6 +348,12 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
   }
 #pragma unroll
   for (int p = 0; p < kChunk / 2; p++) pk[p] = (u[2 * p + 1] << 16) | (u[2 * p] & 0xFFFFu);
+  // bit 16 of each residual only when some lane has one (a wave-uniform branch: rare on most rasters); u >> 16 is
+  // 0 or 1 whenever the kept residuals are used at all (every u < 2^17)
+  if (__any(um > 0xFFFFu)) {
+#pragma unroll
+    for (int jj = 0; jj < kChunk; jj++) hb |= (u[jj] >> 16) << jj;
+  }
   return acc;
 }
 
@@ -702,6 +709,8 @@ k_analyze_w(JobArgs a, int src) {
 #endif
   const int keep_wi = okm ? (FRA_W_KEEP ? 31 - __clz((int)okm) : __builtin_ctz(okm)) : -1;
   bool kept_fit = false;
+  uint64_t hk = 0;  // bit 16 of the kept residuals: bit 16 j + jj = chunk 64 j + lane's residual jj
+  bool hk_any = false;  // (wave-uniform) some kept residual has bit 16
   uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
 #pragma unroll 1
   for (int ci = 0; ci < 2 + nlpc; ci++) {
@@ -740,20 +749,22 @@ k_analyze_w(JobArgs a, int src) {
 #pragma unroll
             for (int k = 0; k < 4; k++) w4[k] = (uint32_t)__builtin_amdgcn_readlane((int)D[6 + k], 0);
           }
-          uint32_t acc = 0, pk[kChunk / 2];
+          uint32_t acc = 0, pk[kChunk / 2], hb = 0;
           switch (o) {
 #define FRA_CASE(O_) \
-  case O_: acc = lpc_abs16_pk<O_>(D, qm, sh, head, pk, um); break;
+  case O_: acc = lpc_abs16_pk<O_>(D, qm, sh, head, pk, um, hb); break;
             FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6) FRA_CASE(7) FRA_CASE(8)
 #undef FRA_CASE
           }
           wsync();  // (all lanes' sample reads of this iteration precede the stores)
 #pragma unroll
           for (int p = 0; p < kChunk / 4; p++) *reinterpret_cast<uint2*>(po + 2 * p) = make_uint2(pk[2 * p], pk[2 * p + 1]);
+          hk |= (uint64_t)hb << (16 * j);
           const uint64_t gs = bperm64(group_sum_auto(2ull * acc, gsl), psrc);
           psum = pj == j ? gs : psum;
         }
-        kept_fit = !__any(um > 0xFFFFu);
+        kept_fit = !__any(um > 0x1FFFFu);  // 16 bits in LDS + bit 16 in hk
+        hk_any = __any(hk != 0);
       } else {
 #pragma unroll 1
         for (int j = 0; j < kWIters; j++) {
@@ -827,7 +838,7 @@ k_analyze_w(JobArgs a, int src) {
     // words may already cover that chunk (calls in order j = 0..3)
     auto residuals = [&](int j, uint32_t (&un)[kChunk], uint32_t (&cy)[6]) {
       const int t = 64 * j + lane;
-      if (kept) {  // 8 dwords of int16 pairs
+      if (kept) {  // 8 dwords of u16 pairs (+ bit 16 of each from hk when the wave has any)
         const uint32_t* po = sw + 8 * lane + kWIterDw * j;
 #pragma unroll
         for (int p = 0; p < kChunk / 4; p++) {
@@ -836,6 +847,11 @@ k_analyze_w(JobArgs a, int src) {
           un[4 * p + 1] = v.x >> 16;
           un[4 * p + 2] = v.y & 0xFFFFu;
           un[4 * p + 3] = v.y >> 16;
+        }
+        if (hk_any) {
+          const uint32_t h = (uint32_t)(hk >> (16 * j));
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) un[jj] |= ((h >> jj) & 1u) << 16;
         }
         return;
       }
@@ -897,6 +913,13 @@ k_analyze_w(JobArgs a, int src) {
           return u16x2{c, c};
         };
         const u16x2 sm = sh(km), s0 = sh(k0), s1 = sh(k0 + 1), mm = wt(km), m0 = wt(k0), m1 = wt(k0 + 1);
+        // bit 16 of a residual adds 2^16 >> k to u >> k (k <= 16; 0 above: u < 2^17): c of them in this chunk
+        if (hk_any) {
+          const uint32_t c = (uint32_t)__builtin_popcount((uint32_t)(hk >> (16 * j)) & 0xFFFFu);
+          f0 = km <= 16 ? c << (16 - km) : 0u;
+          f1 = k0 <= 16 ? c << (16 - k0) : 0u;
+          f2 = k0 + 1 <= 16 ? c << (15 - k0) : 0u;
+        }
 #pragma unroll
         for (int p = 0; p < kChunk / 4; p++) {
           const uint2 v = *reinterpret_cast<const uint2*>(po + 2 * p);
@@ -923,7 +946,7 @@ k_analyze_w(JobArgs a, int src) {
       fk[j][2] = f2;
       k0r[j] = (uint32_t)k0;
       uint64_t v0, v1, v2;
-      if (kept || __all(f0 <= (0xFFFFFFFFu >> ls))) {  // (kept: u < 2^16, so <= 64 lanes fit 32 bits)
+      if (kept || __all(f0 <= (0xFFFFFFFFu >> ls))) {  // (kept: u < 2^17, so <= 64 lanes fit 32 bits)
         v0 = group_sum32(f0, ls); v1 = group_sum32(f1, ls); v2 = group_sum32(f2, ls);
       } else {
         v0 = group_sum64(f0, ls); v1 = group_sum64(f1, ls); v2 = group_sum64(f2, ls);

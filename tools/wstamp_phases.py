@@ -69,7 +69,7 @@ if "--fine" in sys.argv:  # load phase split: 0 -> 10 metadata, 10 -> 11 raw row
     for k, nm in enumerate(["  load: metadata", "  load: raw rows", "  load: LUT gathers + LDS", "  load: reductions"]):
         print(f"{nm:28s} {np.median(dd[:, k]):11.0f} {dd[:, k].mean():10.0f}")
 why = st[:, 9][st[:, 0] > 0]
-names = {1: "partial frame", 2: "no LPC model", 3: "FIXED wins", 4: "other LPC window wins", 5: "residual >= 2^16",
+names = {1: "partial frame", 2: "no LPC model", 3: "FIXED wins", 4: "other LPC window wins", 5: "residual >= 2^17",
          6: "not below VERBATIM", 7: "encode would overrun"}
 hb = {names.get(int(k), str(k)): int((why == k).sum()) for k in np.unique(why) if k}
 print(f"sample-path (non-kept) subframes: {int((why > 0).sum())} of {len(why)} stamped waves: {hb}")
