@@ -474,17 +474,23 @@ k_analyze_w(JobArgs a, int src) {
     wread_d14(sw, lane, j, D);
     int32_t x[28];
     unpack28(D, x);
+    // biased throughout (r05): v = x + 2^31, then each difference order by one v_xad_u32 -- (a ^ 0x7FFFFFFF) + b =
+    // b - a + 2^31 - 1, the next order plus a (new) constant bias that the SAD of two neighbours cancels (|values| <
+    // 2^21: no wrap) -- instead of a subtract and a re-bias per sample and order
+    uint32_t v[28];
+#pragma unroll
+    for (int jx = 8; jx < 28; jx++) v[jx] = (uint32_t)x[jx] ^ kBias;
 #pragma unroll
     for (int k = 0; k <= 4; k++) {
       if (k > 1) {
 #pragma unroll
-        for (int jx = 12 + kChunk - 1; jx >= 7 + k; jx--) x[jx] = x[jx] - x[jx - 1];
+        for (int jx = 12 + kChunk - 1; jx >= 7 + k; jx--) v[jx] = xad_bias(v[jx - 1], v[jx]);
       }
       uint32_t s32 = 0;
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
-        const uint32_t ab = (uint32_t)x[12 + jj] ^ kBias;
-        const uint32_t bb = k == 0 ? kBias : ((jj < k && head) ? ab : (uint32_t)x[11 + jj] ^ kBias);
+        const uint32_t ab = v[12 + jj];
+        const uint32_t bb = k == 0 ? kBias : ((jj < k && head) ? ab : v[11 + jj]);
         s32 = sad_acc(ab, bb, s32);
       }
       // a partition of <= 512 samples: 2 sum |r| < 2^30

@@ -564,6 +564,12 @@ __device__ __forceinline__ uint32_t sad_acc(uint32_t ab, uint32_t bb, uint32_t a
   asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(ab), "v"(bb), "v"(acc));
   return d;
 }
+// b - a + 2^31 - 1 (mod 2^32) in one v_xad_u32: the biased difference of two values of the same bias
+__device__ __forceinline__ uint32_t xad_bias(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(0x7FFFFFFFu), "v"(b));
+  return d;
+}
 __device__ __forceinline__ uint64_t abs2_64(int64_t r) { return 2 * (uint64_t)(r < 0 ? -r : r); }
 __device__ __forceinline__ int bitlen64(uint64_t v) { return v ? 64 - __clzll((long long)v) : 0; }
 
