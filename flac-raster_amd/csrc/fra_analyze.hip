@@ -534,17 +534,21 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
     // order k residual at j = the (k-1)-th difference x[j] - x[j-1]; |.| by v_sad_u32 on biased values
     // (x holds the (k-1)-th difference for j >= 7 + k); warm-up samples 0..k-1 belong to thread 0
     // (i0 == 0): those k positions compare a value with itself
+    // (r05: kept biased, each difference order by one v_xad_u32 -- xad_bias, as in k_analyze_w)
+    uint32_t v[12 + kChunk];
+#pragma unroll
+    for (int j = 8; j < 12 + kChunk; j++) v[j] = (uint32_t)x[j] ^ kBias;
 #pragma unroll
     for (int k = 0; k <= 4; k++) {
       if (k > 1) {
 #pragma unroll
-        for (int j = 12 + kChunk - 1; j >= 7 + k; j--) x[j] = x[j] - x[j - 1];
+        for (int j = 12 + kChunk - 1; j >= 7 + k; j--) v[j] = xad_bias(v[j - 1], v[j]);
       }
       uint32_t s32 = 0;
 #pragma unroll
       for (int jj = 0; jj < kChunk; jj++) {
-        const uint32_t ab = (uint32_t)x[12 + jj] ^ kBias;
-        const uint32_t bb = k == 0 ? kBias : ((jj < k && head) ? ab : (uint32_t)x[11 + jj] ^ kBias);
+        const uint32_t ab = v[12 + jj];
+        const uint32_t bb = k == 0 ? kBias : ((jj < k && head) ? ab : v[11 + jj]);
         s32 = sad_acc(ab, bb, s32);
       }
       if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], 2ull * s32);
