@@ -82,6 +82,15 @@ struct fra_ctx {
   std::vector<hipStream_t> stage_st;
 };
 
+// Pipelined execute: does the norm stage of execute k wait for the assembly of execute k-2 (one background kernel
+// at a time beside the analysis)?  16-bit plans: no -- the norm stage then runs beside that assembly and the
+// analysis of execute k-1 (C4 step 1.526 -> 1.497-1.504 ms, its 8-way shares -4 %, C3 -0.8 %); 32-bps plans:
+// yes (C5 quarter +0.4 % without) -- profiles/r05_ab_bg_serial.txt.  FRA_BG_SERIAL=0/1 overrides (A/B)
+static bool bg_serial(bool b32) {
+  static const int v = getenv("FRA_BG_SERIAL") ? atoi(getenv("FRA_BG_SERIAL")) : -1;
+  return v < 0 ? b32 : v == 1;
+}
+
 struct fra_plan {
   fra_ctx* ctx = nullptr;
   fra_job job{};
@@ -1013,6 +1022,9 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     HIPCHK(hipEventRecord(ev_norm, norm_st));
     HIPCHK(hipStreamWaitEvent(st, ev_norm, 0));
     if (ev_part) {
+      // (these slots: execute k-2's assembly read them -- the norm stream waited for it, or, FRA_BG_SERIAL=0,
+      // this stream does just before the launch)
+      if (!bg_serial(p->b32) && p->pack_pending[p->cur]) HIPCHK(hipStreamWaitEvent(norm_st, p->ev_pack[p->cur], 0));
       HIPCHK(launch_analyze_part(p->src, p->b32, ga, part, npart, 8 * p->ncu, norm_st));
       HIPCHK(hipEventRecord(ev_part, norm_st));
     }
@@ -1073,8 +1085,11 @@ int fra_plan_execute(fra_plan* p) {
     const hipStream_t as = p->astream[b] ? p->astream[b] : s;  // this execute's analysis stream
     if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(as, p->ev_pack[b], 0));  // execute k-2 is done with set b
     // one background kernel at a time beside k_analyze: this norm stage after k_assemble of execute k-2
-    // (which runs under the analysis of execute k-1)
-    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_pack[b], 0));
+    // (which runs under the analysis of execute k-1) -- 32-bps plans; 16-bit plans: only the partial-subframe list launch
+    // after the norm stage waits for that assembly (it rewrites the slots; the norm stage writes only this set's
+    // NormDev / table, which execute k-2's analysis and partial list -- both earlier on this stream or waited
+    // for below -- read)
+    if (p->pack_pending[b] && bg_serial(p->b32)) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_pack[b], 0));
     use_buffers(p, b);
     // norm stage of this execute on the norm stream: after execute k-2's analysis read set b, and after a
     // host raster copy enqueued on the plan's stream since the last execute
