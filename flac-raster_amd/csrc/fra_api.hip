@@ -182,8 +182,16 @@ struct fra_plan {
   // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Neither analysis
   // leaves room beside it (k_analyze_w: 20 waves x 8 KiB fill the CU's LDS; 32-bps k_analyze: 5 workgroups of
   // 31.6 KiB), so the background kernels run in the gaps between analysis waves
-  NormDev* norm2[2] = {};
-  int32_t* lut2[2] = {};
+  // norm sets (NormDev + table) cycle over kNormSets executes, the slot sets above over 2 (r05): execute k+1's norm
+  // stage waits for execute k-2's analysis, not k-1's, so the norm stream runs up to a whole execute ahead and
+  // execute k+1's table is ready before execute k's analysis drains (its waves fill that grid's last, partly empty
+  // generation instead of waiting behind a k_minmax_vec that runs ~1.1 ms beside the analysis)
+  static constexpr int kNormSets = 3;
+  NormDev* norm2[kNormSets] = {};
+  int32_t* lut2[kNormSets] = {};
+  int curn = 0;  // norm set of the last pipelined execute
+  hipEvent_t ev_nfree[kNormSets] = {};  // the last analysis (+ partial list) reading norm set n is done
+  bool nfree_pending[kNormSets] = {};
   hipStream_t nstream = nullptr;
   hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
   bool ana_pending[2] = {false, false};
@@ -356,8 +364,11 @@ void fra_plan_destroy(fra_plan* p) {
       (void)hipFree(p->foff2[b]);
       (void)hipFree(p->tmp2[b]);
       (void)hipFree(p->fmeta2[b]);
-      (void)hipFree(p->norm2[b]);
-      (void)hipFree(p->lut2[b]);
+    }
+    for (int n = 0; n < fra_plan::kNormSets; n++) {
+      (void)hipFree(p->norm2[n]);
+      (void)hipFree(p->lut2[n]);
+      if (p->ev_nfree[n]) (void)hipEventDestroy(p->ev_nfree[n]);
     }
     p->d_sf = nullptr; p->d_fbytes = nullptr; p->d_foff = nullptr; p->d_tmp = nullptr; p->d_fmeta = nullptr;
     p->d_norm = nullptr; p->d_lut = nullptr;
@@ -776,16 +787,19 @@ static int plan_build(fra_plan* p) {
     const size_t nst = std::max<size_t>(1, p->streams.size());
     const size_t extra = sizeof(SfDesc) * nsf + sizeof(uint32_t) * (size_t)p->tmp_stride * nsf +
                          sizeof(uint32_t) * kMetaWords * nfr + 2 * sizeof(unsigned long long) * (nfr + 1) +
-                         sizeof(NormDev) * nst + (p->d_lut ? sizeof(int32_t) * (size_t)lut_stride * nst : 0);
+                         (fra_plan::kNormSets - 1) * (sizeof(NormDev) * nst + (p->d_lut ? sizeof(int32_t) * (size_t)lut_stride * nst : 0));
     size_t freeb = 0, totalb = 0;
     if (want && hipMemGetInfo(&freeb, &totalb) == hipSuccess && extra <= freeb / 3) {
       p->sf2[0] = p->d_sf; p->tmp2[0] = p->d_tmp; p->fmeta2[0] = p->d_fmeta;
       p->fbytes2[0] = p->d_fbytes; p->foff2[0] = p->d_foff;
       p->norm2[0] = p->d_norm; p->lut2[0] = p->d_lut;
       p->pipe = true;  // from here on destroy frees through the arrays
-      HIPCHK(hipMalloc(&p->norm2[1], sizeof(NormDev) * nst));
-      HIPCHK(hipMemset(p->norm2[1], 0, sizeof(NormDev) * nst));
-      if (p->d_lut) HIPCHK(hipMalloc(&p->lut2[1], sizeof(int32_t) * (size_t)lut_stride * nst));
+      for (int n = 1; n < fra_plan::kNormSets; n++) {
+        HIPCHK(hipMalloc(&p->norm2[n], sizeof(NormDev) * nst));
+        HIPCHK(hipMemset(p->norm2[n], 0, sizeof(NormDev) * nst));
+        if (p->d_lut) HIPCHK(hipMalloc(&p->lut2[n], sizeof(int32_t) * (size_t)lut_stride * nst));
+      }
+      for (auto& e : p->ev_nfree) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       {  // background streams at the lowest priority (the plan's stream is created at the highest)
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -819,15 +833,16 @@ static int plan_build(fra_plan* p) {
 }
 
 // point the plan (and its kernel arguments) at buffer set b
-static void use_buffers(fra_plan* p, int b) {
+static void use_buffers(fra_plan* p, int b, int nb) {
   if (!p->pipe) return;
   p->d_sf = p->sf2[b]; p->d_tmp = p->tmp2[b]; p->d_fmeta = p->fmeta2[b];
   p->d_fbytes = p->fbytes2[b]; p->d_foff = p->foff2[b];
-  p->d_norm = p->norm2[b]; p->d_lut = p->lut2[b];
+  p->d_norm = p->norm2[nb]; p->d_lut = p->lut2[nb];
   p->args.sf = p->d_sf; p->args.tmp = p->d_tmp; p->args.fmeta = p->d_fmeta; p->args.err = p->d_err;
   p->args.frame_bytes = p->d_fbytes; p->args.frame_off = p->d_foff;
   p->args.norm = p->d_norm; p->args.lut = p->d_lut;
   p->cur = b;
+  p->curn = nb;
 }
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
@@ -842,13 +857,17 @@ static int drain_pipeline(fra_plan* p) {
     if (p->ana_pending[b] && p->astream[b]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
     p->ana_pending[b] = false;  // (covered by the resync below)
   }
+  for (int n = 0; n < fra_plan::kNormSets; n++) {  // (norm stream: its partial-subframe lists)
+    if (p->nfree_pending[n]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_nfree[n], 0));
+    p->nfree_pending[n] = false;
+  }
   // serial executes and host raster copies now go onto the plan's stream; when pipelining resumes, the
   // first background norm stage waits for ALL of it (an event recorded on the plan's stream at that
   // point): a pipelined analysis still reading a norm set or a raster copy queued before this drain
   // cannot be overtaken
   p->resync = true;
   p->raster_dirty = false;
-  use_buffers(p, 0);
+  use_buffers(p, 0, 0);
   return FRA_OK;
 }
 static int plan_sync_all(fra_plan* p) {
@@ -1090,10 +1109,14 @@ int fra_plan_execute(fra_plan* p) {
     // NormDev / table, which execute k-2's analysis and partial list -- both earlier on this stream or waited
     // for below -- read)
     if (p->pack_pending[b] && bg_serial(p->b32)) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_pack[b], 0));
-    use_buffers(p, b);
-    // norm stage of this execute on the norm stream: after execute k-2's analysis read set b, and after a
-    // host raster copy enqueued on the plan's stream since the last execute
-    if (p->ana_pending[b]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_ana[b], 0));
+    // norm set: the next of kNormSets (FRA_NORM_SETS=2: the slot set's, as before r05 -- A/B)
+    static const int nsets = getenv("FRA_NORM_SETS") && atoi(getenv("FRA_NORM_SETS")) == 2 ? 2 : fra_plan::kNormSets;
+    const int nb = nsets == 2 ? b : (p->curn + 1) % fra_plan::kNormSets;
+    use_buffers(p, b, nb);
+    // norm stage of this execute on the norm stream: after the last analysis that read norm set nb (execute
+    // k-3, or k-2 with two sets), and after a host raster copy enqueued on the plan's stream since the last
+    // execute.  (That analysis's partial-subframe list ran earlier on the norm stream itself.)
+    if (p->nfree_pending[nb]) HIPCHK(hipStreamWaitEvent(p->nstream, p->ev_nfree[nb], 0));
     if (p->resync) {  // first pipelined execute after serial ones: after everything on the plan's stream
       HIPCHK(hipEventRecord(p->ev_raster, s));
       for (auto& st : p->astream)
@@ -1109,6 +1132,8 @@ int fra_plan_execute(fra_plan* p) {
                    p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
     if (rc) return rc;
     p->ana_pending[b] = true;
+    HIPCHK(hipEventRecord(p->ev_nfree[nb], as));  // (the analysis was the last work on `as`)
+    p->nfree_pending[nb] = true;
     HIPCHK(hipEventRecord(p->ev_pack[b], p->pack));
     p->pack_pending[b] = true;
     p->executed = true;

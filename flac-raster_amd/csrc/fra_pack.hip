@@ -7,6 +7,9 @@
 #include "fra_assemble.h"
 
 namespace fra {
+#ifndef FRA_ASM_U
+#define FRA_ASM_U 2
+#endif
 
 // four frames per workgroup, one per wave -- the 17.5 KiB of CRC tables are copied to LDS
 // once for four frames (a C3 frame is only ~7 KiB) and a frame needs no workgroup barrier.  r03 v20: C4
@@ -17,7 +20,7 @@ __global__ void __launch_bounds__(kThreads, 8) k_assemble4(JobArgs a) {
   copy_tables(a, S);
   __syncthreads();
   const int i = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  if (i < a.frame_count) assemble_frame<2>(a, a.frame_base + i, S);
+  if (i < a.frame_count) assemble_frame<FRA_ASM_U>(a, a.frame_base + i, S);
 }
 
 hipError_t launch_assemble(const JobArgs& a, hipStream_t s) {
