@@ -125,7 +125,7 @@ struct fra_plan {
   bool wave_ok = false;
   hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
   hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
-  hipEvent_t ev_part[2] = {};  // pipelined: the partial subframes of buffer set b done (on the norm stream)
+  hipEvent_t ev_part[3] = {};  // pipelined: the partial subframes of buffer set b done (on the norm stream)
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
   unsigned long long* d_foff = nullptr;
@@ -166,18 +166,23 @@ struct fra_plan {
   // while the frame-size chain + assembly of execute k-1 (reading the other set) run on the pack stream
   bool pipe = false;
   int cur = 0;  // buffer set of the last execute
-  SfDesc* sf2[2] = {};
-  uint32_t* tmp2[2] = {};
-  uint32_t* fmeta2[2] = {};
-  unsigned long long* fbytes2[2] = {};
-  unsigned long long* foff2[2] = {};
+  // slot sets (descriptors, encoded-subframe slots, frame sizes / offsets): nslot = 2, or 3 (FRA_SLOT_SETS=3: execute
+  // k's analysis then waits for the assembly of execute k-3 instead of k-2); the analysis streams alternate by execute
+  static constexpr int kSlotSets = 3;
+  int nslot = 2;
+  unsigned exec_n = 0;
+  SfDesc* sf2[kSlotSets] = {};
+  uint32_t* tmp2[kSlotSets] = {};
+  uint32_t* fmeta2[kSlotSets] = {};
+  unsigned long long* fbytes2[kSlotSets] = {};
+  unsigned long long* foff2[kSlotSets] = {};
   hipStream_t pack = nullptr;
   // the analysis of buffer set b runs on astream[b] (highest priority): execute k+1's k_analyze is queued
   // on the other stream than execute k's, so its first workgroups fill the CUs that execute k's tail
   // leaves idle instead of waiting for that kernel to end
   hipStream_t astream[2] = {};
-  hipEvent_t ev_scan[2] = {}, ev_pack[2] = {};
-  bool pack_pending[2] = {false, false};
+  hipEvent_t ev_scan[kSlotSets] = {}, ev_pack[kSlotSets] = {};
+  bool pack_pending[kSlotSets] = {};
   // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
   // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Neither analysis
   // leaves room beside it (k_analyze_w: 20 waves x 8 KiB fill the CU's LDS; 32-bps k_analyze: 5 workgroups of
@@ -193,8 +198,8 @@ struct fra_plan {
   hipEvent_t ev_nfree[kNormSets] = {};  // the last analysis (+ partial list) reading norm set n is done
   bool nfree_pending[kNormSets] = {};
   hipStream_t nstream = nullptr;
-  hipEvent_t ev_norm[2] = {}, ev_ana[2] = {}, ev_raster = nullptr;
-  bool ana_pending[2] = {false, false};
+  hipEvent_t ev_norm[kSlotSets] = {}, ev_ana[kSlotSets] = {}, ev_raster = nullptr;
+  bool ana_pending[kSlotSets] = {};
   bool raster_dirty = false;  // a host raster copy on the plan's stream the norm stream must wait for
   bool resync = false;        // serial work was queued on the plan's stream since the last pipelined execute
   // timing
@@ -358,7 +363,7 @@ void fra_plan_destroy(fra_plan* p) {
   for (auto e : p->ev_part)
     if (e) (void)hipEventDestroy(e);
   if (p->pipe) {  // d_* alias set 0 or 1: free both sets through the arrays
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < fra_plan::kSlotSets; b++) {
       (void)hipFree(p->sf2[b]);
       (void)hipFree(p->fbytes2[b]);
       (void)hipFree(p->foff2[b]);
@@ -377,7 +382,7 @@ void fra_plan_destroy(fra_plan* p) {
   if (p->nstream) (void)hipStreamDestroy(p->nstream);
   for (auto& st : p->astream)
     if (st) (void)hipStreamDestroy(st);
-  for (int b = 0; b < 2; b++) {
+  for (int b = 0; b < fra_plan::kSlotSets; b++) {
     if (p->ev_scan[b]) (void)hipEventDestroy(p->ev_scan[b]);
     if (p->ev_pack[b]) (void)hipEventDestroy(p->ev_pack[b]);
     if (p->ev_norm[b]) (void)hipEventDestroy(p->ev_norm[b]);
@@ -806,11 +811,18 @@ static int plan_build(fra_plan* p) {
         HIPCHK(hipStreamCreateWithPriority(&p->nstream, hipStreamNonBlocking, lo));
       }
       HIPCHK(hipEventCreateWithFlags(&p->ev_raster, hipEventDisableTiming));
-      HIPCHK(hipMalloc(&p->sf2[1], sizeof(SfDesc) * std::max<size_t>(1, nsf)));
-      HIPCHK(hipMalloc(&p->tmp2[1], sizeof(uint32_t) * (size_t)p->tmp_stride * std::max<size_t>(1, nsf)));
-      HIPCHK(hipMalloc(&p->fmeta2[1], sizeof(uint32_t) * kMetaWords * nfr));
-      HIPCHK(hipMalloc(&p->fbytes2[1], sizeof(unsigned long long) * (nfr + 1)));
-      HIPCHK(hipMalloc(&p->foff2[1], sizeof(unsigned long long) * (nfr + 1)));
+      {
+        static const int want3 = getenv("FRA_SLOT_SETS") ? atoi(getenv("FRA_SLOT_SETS")) : 2;  // A/B
+        size_t f2 = 0, t2 = 0;
+        p->nslot = (want3 == 3 && hipMemGetInfo(&f2, &t2) == hipSuccess && 2 * extra <= f2 / 3) ? 3 : 2;
+      }
+      for (int b = 1; b < p->nslot; b++) {
+        HIPCHK(hipMalloc(&p->sf2[b], sizeof(SfDesc) * std::max<size_t>(1, nsf)));
+        HIPCHK(hipMalloc(&p->tmp2[b], sizeof(uint32_t) * (size_t)p->tmp_stride * std::max<size_t>(1, nsf)));
+        HIPCHK(hipMalloc(&p->fmeta2[b], sizeof(uint32_t) * kMetaWords * nfr));
+        HIPCHK(hipMalloc(&p->fbytes2[b], sizeof(unsigned long long) * (nfr + 1)));
+        HIPCHK(hipMalloc(&p->foff2[b], sizeof(unsigned long long) * (nfr + 1)));
+      }
       {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -820,7 +832,7 @@ static int plan_build(fra_plan* p) {
         // profiles/r04_ab_dual_streams_32bps.txt)
         for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
       }
-      for (int b = 0; b < 2; b++) {
+      for (int b = 0; b < fra_plan::kSlotSets; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&p->ev_pack[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&p->ev_norm[b], hipEventDisableTiming));
@@ -847,14 +859,14 @@ static void use_buffers(fra_plan* p, int b, int nb) {
 // make the plan's stream wait for every k_assemble still running on the pack stream, then use set 0
 static int drain_pipeline(fra_plan* p) {
   if (!p->pipe) return FRA_OK;
-  for (int b = 0; b < 2; b++) {
+  for (int b = 0; b < fra_plan::kSlotSets; b++) {
     if (p->pack_pending[b]) {
       HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_pack[b], 0));
       p->pack_pending[b] = false;
     }
     // (an analysis on astream[b] is followed by its chain + assembly on the pack stream: covered above;
     // the wait below also orders a pipelined execute's analysis before the serial work that follows)
-    if (p->ana_pending[b] && p->astream[b]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
+    if (p->ana_pending[b] && p->astream[0]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
     p->ana_pending[b] = false;  // (covered by the resync below)
   }
   for (int n = 0; n < fra_plan::kNormSets; n++) {  // (norm stream: its partial-subframe lists)
@@ -895,8 +907,8 @@ int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
   } else {
     if (!p->d_raster_owned && p->raster_bytes) HIPCHK(hipMalloc(&p->d_raster_owned, p->raster_bytes));
     // the copy must not overtake a pipelined analysis (its own stream) still reading the old rows
-    for (int b = 0; b < 2; b++)
-      if (p->ana_pending[b] && p->astream[b]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
+    for (int b = 0; b < fra_plan::kSlotSets; b++)
+      if (p->ana_pending[b] && p->astream[0]) HIPCHK(hipStreamWaitEvent(p->ctx->stream, p->ev_ana[b], 0));
     if (p->raster_bytes) {
       HIPCHK(hipMemcpyAsync(p->d_raster_owned, raster, p->raster_bytes, hipMemcpyHostToDevice, p->ctx->stream));
       if (p->pipe) {  // the next pipelined norm stage (norm stream) reads the new raster after this copy
@@ -1100,9 +1112,10 @@ int fra_plan_execute(fra_plan* p) {
   int rc = FRA_OK;
   if (p->pipe && !p->timing) {
     // cross-execute pipelining: this execute's analysis overlaps the previous execute's k_assemble
-    const int b = p->cur ^ 1;
-    const hipStream_t as = p->astream[b] ? p->astream[b] : s;  // this execute's analysis stream
-    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(as, p->ev_pack[b], 0));  // execute k-2 is done with set b
+    const int b = (p->cur + 1) % p->nslot;
+    const int ai = (int)(p->exec_n++ & 1u);
+    const hipStream_t as = p->astream[ai] ? p->astream[ai] : s;  // this execute's analysis stream
+    if (p->pack_pending[b]) HIPCHK(hipStreamWaitEvent(as, p->ev_pack[b], 0));  // execute k-nslot is done with set b
     // one background kernel at a time beside k_analyze: this norm stage after k_assemble of execute k-2
     // (which runs under the analysis of execute k-1) -- 32-bps plans; 16-bit plans: only the partial-subframe list launch
     // after the norm stage waits for that assembly (it rewrites the slots; the norm stage writes only this set's
