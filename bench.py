@@ -270,7 +270,7 @@ def inrun_pmc(args, kernel):
     return res
 
 
-def analysis_kernel(cfg, dt, wave):
+def analysis_kernel(cfg, dt, wave, k17=True):
     """(label, mangled-name prefix) of the analysis kernel a plan of this config launches: k_analyze_w when the plan
     reports FRA_PLAN_WAVE (``wave``: full frames one subframe per wave, the partial-frame list on k_analyze beside
     it) for a <= 16-bit raster, else the k_analyze instance of the sample width and the level's lag."""
@@ -278,7 +278,7 @@ def analysis_kernel(cfg, dt, wave):
     if wave and np.dtype(dt).itemsize <= 2:
         pcap = {3: 4, 4: 4, 5: 5, 6: 6}[lvl]
         return ("k_analyze_w (+ k_analyze over the partial-frame list, same phase)",
-                f"_ZN3fra11k_analyze_wILi8ELi{pcap}E")
+                f"_ZN3fra11k_analyze_wILi8ELi{pcap}ELb{1 if k17 else 0}E")
     b32 = 1 if cfg["norm"] == 24 or np.dtype(dt).itemsize > 2 else 0
     lag = 12 if lvl >= 7 else (8 if lvl >= 3 else 0)
     return "k_analyze", f"_ZN3fra9k_analyzeILb{b32}ELi{lag}E"
@@ -468,6 +468,7 @@ def main():
     plan = N.Plan(ctx, dev_raster, True, dt, B, (H * W, W, 1), my_wins, cfg["level"], 4096, cfg["norm"],
                   frame_ranges=ranges)
     wave_plan = bool(plan.flags() & 4)  # FRA_PLAN_WAVE: full frames on k_analyze_w
+    k17_plan = True
 
     if args.child:  # rocprofv3 child: the plan's launches only
         if args.child_serial:  # the roofline's mode: serial executes, each kernel alone on the device
@@ -499,6 +500,8 @@ def main():
     kms, nexec = plan.timing()
     plan.enable_timing(False)
     infos, total = plan.result()
+    # the k_analyze_w instance the plan settled on (FRA_PLAN_KEEP17: kept residuals up to 17 bits, else 16)
+    k17_plan = bool(plan.flags() & 8)
     # pixels of this rank's frames (a partial tile counts its frame range only)
     my_px = sum(min(wins[i][2] * wins[i][3], (f0 + n) * 4096) - f0 * 4096 for i, f0, n in items)
     my_in_bytes = my_px * B * dt.itemsize
@@ -620,7 +623,7 @@ def main():
         dom_label = dom_name
         codegen = codegen_stats(dom_name)
         if dom_name == "k_analyze":
-            dom_label, prefix = analysis_kernel(cfg, dt, wave_plan)
+            dom_label, prefix = analysis_kernel(cfg, dt, wave_plan, k17_plan)
             codegen = codegen_stats(prefix.split("ILb")[0].split("ILi")[0].rsplit("fra", 1)[1].lstrip("0123456789"),
                                     prefix)
         hbm_frac = achieved / HBM_PEAK_GBPS

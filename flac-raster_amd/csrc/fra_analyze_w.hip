@@ -328,7 +328,7 @@ __device__ __forceinline__ uint32_t lpc_abs16_w(const uint32_t (&D)[14], const i
 
 // the same sum, plus the chunk's zig-zag residuals packed two per dword (u[2p] low, u[2p+1] high: their low 16
 // bits) and bit 16 of each in `hb` (bit jj; r05): exact whenever every u < 2^17, which `um`, the OR of all u, tells
-template <int O>
+template <int O, bool K17>
 __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const int32_t* q, int sh, bool head,
                                                  uint32_t (&pk)[kChunk / 2], uint32_t& um, uint32_t& hb) {
   constexpr int NP = (O + 1) / 2;
@@ -350,7 +350,7 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
   for (int p = 0; p < kChunk / 2; p++) pk[p] = (u[2 * p + 1] << 16) | (u[2 * p] & 0xFFFFu);
   // bit 16 of each residual only when some lane has one (a wave-uniform branch: rare on most rasters); u >> 16 is
   // 0 or 1 whenever the kept residuals are used at all (every u < 2^17)
-  if (__any(um > 0xFFFFu)) {
+  if (K17 && __any(um > 0xFFFFu)) {
 #pragma unroll
     for (int jj = 0; jj < kChunk; jj++) hb |= (u[jj] >> 16) << jj;
   }
@@ -366,7 +366,11 @@ __device__ __forceinline__ uint32_t lpc_abs16_pk(const uint32_t (&D)[14], const 
 // always search orders PCAP..0 (4096 >> 7 > 8 = max order), so the group / node loops of the FIXED sums, the LPC
 // sums and the partition search are straight code instead of uniform branches on a runtime order -- branches
 // that also split the blocks the scheduler could otherwise overlap the ds_bpermute round trips in
-template <int MAXLAG, int PCAP>
+// K17 (r05): kept residuals up to 17 bits (true) or 16 (false: the bit-16 masks and their corrections compiled out,
+// 97 instead of 110 VGPRs, which leaves the background kernels of a pipelined execute room beside the analysis).
+// The plan picks the instance per execute from the count of waves whose kept residuals needed bit 16 in an earlier
+// execute (JobArgs::cnt17, both instances count them); the bytes are the same either way (FRA-1)
+template <int MAXLAG, int PCAP, bool K17>
 // occupancy target: 4 waves per SIMD (r05).  8 KiB of LDS would let 20 waves share a CU and <= 96 VGPRs make it 5 per
 // SIMD, but at 4 (97 VGPRs here) the CU keeps 32 KiB of LDS and a wave slot per SIMD for the norm stage and the
 // assembly of the neighbouring executes, which then run beside the analysis instead of in its gaps: C4 step
@@ -758,7 +762,7 @@ k_analyze_w(JobArgs a, int src) {
           uint32_t acc = 0, pk[kChunk / 2], hb = 0;
           switch (o) {
 #define FRA_CASE(O_) \
-  case O_: acc = lpc_abs16_pk<O_>(D, qm, sh, head, pk, um, hb); break;
+  case O_: acc = lpc_abs16_pk<O_, K17>(D, qm, sh, head, pk, um, hb); break;
             FRA_CASE(1) FRA_CASE(2) FRA_CASE(3) FRA_CASE(4) FRA_CASE(5) FRA_CASE(6) FRA_CASE(7) FRA_CASE(8)
 #undef FRA_CASE
           }
@@ -769,8 +773,14 @@ k_analyze_w(JobArgs a, int src) {
           const uint64_t gs = bperm64(group_sum_auto(2ull * acc, gsl), psrc);
           psum = pj == j ? gs : psum;
         }
-        kept_fit = !__any(um > 0x1FFFFu);  // 16 bits in LDS + bit 16 in hk
-        hk_any = __any(hk != 0);
+        const bool need17 = __any(um > 0xFFFFu) && !__any(um > 0x1FFFFu);  // (wave-uniform)
+        if (need17 && lane == 0 && a.cnt17) atomicAdd(a.cnt17, 1u);  // (a vector atomic: lane 0 only)
+        if constexpr (K17) {
+          kept_fit = !__any(um > 0x1FFFFu);  // 16 bits in LDS + bit 16 in hk
+          hk_any = __any(hk != 0);
+        } else {
+          kept_fit = !__any(um > 0xFFFFu);
+        }
       } else {
 #pragma unroll 1
         for (int j = 0; j < kWIters; j++) {
@@ -1181,15 +1191,16 @@ namespace fra {
 #endif
 
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s) {
+  const bool k17 = a.k17 != 0;
   if (a.frame_count <= 0) return hipSuccess;
   const dim3 grid((unsigned)a.frame_count, (unsigned)cw);
   const LevelCfg cfg = level_cfg(level);
   if (cfg.nsub == 0 || cfg.max_lpc > 8) return hipErrorInvalidValue;  // levels 3-6 only
   if (!a.wave) return hipErrorInvalidValue;  // the plan's per-frame descriptors (wave-path plans)
   switch (cfg.max_porder) {
-    case 4: k_analyze_w<8, 4><<<grid, 64, 0, s>>>(a, src); break;
-    case 5: k_analyze_w<8, 5><<<grid, 64, 0, s>>>(a, src); break;
-    default: k_analyze_w<8, 6><<<grid, 64, 0, s>>>(a, src); break;
+    case 4: k17 ? k_analyze_w<8, 4, true><<<grid, 64, 0, s>>>(a, src) : k_analyze_w<8, 4, false><<<grid, 64, 0, s>>>(a, src); break;
+    case 5: k17 ? k_analyze_w<8, 5, true><<<grid, 64, 0, s>>>(a, src) : k_analyze_w<8, 5, false><<<grid, 64, 0, s>>>(a, src); break;
+    default: k17 ? k_analyze_w<8, 6, true><<<grid, 64, 0, s>>>(a, src) : k_analyze_w<8, 6, false><<<grid, 64, 0, s>>>(a, src); break;
   }
   return hipGetLastError();
 }

@@ -125,6 +125,21 @@ struct fra_plan {
   bool wave_ok = false;
   hipStream_t pside = nullptr;  // the partial subframes' stream (beside k_analyze_w) and its fork / join
   hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+  // k_analyze_w instance (r05): kept residuals up to 17 bits or 16 (JobArgs::k17), picked per execute from how many
+  // waves of an earlier execute needed bit 16.  Pipelined plans count into d_cnt17[j] (ring slot j of kCnt, never
+  // reset: an execute's count is its snapshot minus the slot's previous one) and copy the counter into page-locked
+  // h_cnt17[j] after the analysis; the host reads a snapshot once its event has completed (no sync)
+  static constexpr int kCnt = 4;
+  uint32_t* d_cnt17 = nullptr;
+  uint32_t* h_cnt17 = nullptr;
+  uint32_t cnt_base[kCnt] = {};
+  hipEvent_t ev_cnt[kCnt] = {};
+  bool cnt_pending[kCnt] = {};
+  uint64_t cnt_seq[kCnt] = {};
+  uint32_t cnt_sub[kCnt] = {};
+  uint64_t cnt_next = 0, cnt_newest = 0;
+  int cnt_cur = -1;  // the counter slot the last run_group launch counted into (-1: none)
+  int k17 = 1;  // start with 17 bits: never slower than the sample path by more than its VGPR cost
   hipEvent_t ev_part[3] = {};  // pipelined: the partial subframes of buffer set b done (on the norm stream)
   SfDesc* d_sf = nullptr;
   unsigned long long* d_fbytes = nullptr;
@@ -409,6 +424,10 @@ void fra_plan_destroy(fra_plan* p) {
     if (e) (void)hipEventDestroy(e);
   if (p->hev_start) (void)hipEventDestroy(p->hev_start);
   if (p->h_gbase) (void)hipHostFree(p->h_gbase);
+  if (p->h_cnt17) (void)hipHostFree(p->h_cnt17);
+  (void)hipFree(p->d_cnt17);
+  for (auto e : p->ev_cnt)
+    if (e) (void)hipEventDestroy(e);
   for (auto& e : p->gev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : p->ev)
@@ -831,6 +850,12 @@ static int plan_build(fra_plan* p) {
         // early start displaced is gone (r03: C5 +5 % with it; r04: C5 106.50 -> 106.24 ms,
         // profiles/r04_ab_dual_streams_32bps.txt)
         for (int b = 0; b < 2; b++) HIPCHK(hipStreamCreateWithPriority(&p->astream[b], hipStreamNonBlocking, hi));
+        if (p->wave_ok) {  // the k_analyze_w instance counters (fra_plan::kCnt ring)
+          HIPCHK(hipMalloc(&p->d_cnt17, sizeof(uint32_t) * fra_plan::kCnt));
+          HIPCHK(hipMemset(p->d_cnt17, 0, sizeof(uint32_t) * fra_plan::kCnt));
+          HIPCHK(hipHostMalloc((void**)&p->h_cnt17, sizeof(uint32_t) * fra_plan::kCnt, hipHostMallocPortable));
+          for (auto& e : p->ev_cnt) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
       }
       for (int b = 0; b < fra_plan::kSlotSets; b++) {
         HIPCHK(hipEventCreateWithFlags(&p->ev_scan[b], hipEventDisableTiming));
@@ -1061,12 +1086,36 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
     }
   }
   if (t_norm) HIPCHK(hipEventRecord(t_norm, st));
+  int cj = -1;  // the counter slot of this launch (-1: not counted)
+  if (wave) {
+    // the snapshots that have arrived (newest wins): 17 bits when more than 1/32 of its waves needed bit 16 -- a wave
+    // that does on the 16-bit instance re-derives its residuals from the samples (the sample path)
+    for (int j = 0; j < fra_plan::kCnt; j++) {
+      if (!p->cnt_pending[j] || hipEventQuery(p->ev_cnt[j]) != hipSuccess) continue;
+      p->cnt_pending[j] = false;
+      const uint32_t n17 = p->h_cnt17[j] - p->cnt_base[j];
+      p->cnt_base[j] = p->h_cnt17[j];
+      if (p->cnt_seq[j] >= p->cnt_newest) {
+        p->cnt_newest = p->cnt_seq[j];
+        p->k17 = n17 > p->cnt_sub[j] / 32 ? 1 : 0;
+      }
+    }
+    const char* ek = getenv("FRA_KEEP17");  // tests / A/B: 0 or 1 forces the instance
+    ga.k17 = (ek && ek[0] == '0') ? 0 : (ek && ek[0] == '1') ? 1 : p->k17;
+    const int j = (int)(p->cnt_next % fra_plan::kCnt);
+    if (p->d_cnt17 && !p->cnt_pending[j] && nf > 0 && ng == 1) {
+      cj = j;
+      ga.cnt17 = p->d_cnt17 + j;
+    }
+  }
+  p->cnt_cur = cj;  // (fra_plan_execute copies the count out after everything the execute timed or waits on)
   {
     HIPCHK(launch_analyze(p->src, p->b32, p->cmax == 4 && p->job.channels == 2, ga, st, wave,
                           ev_part ? nullptr : part, ev_part ? 0 : npart, 8 * p->ncu, p->pside, p->ev_pfork,
                           p->ev_pjoin));
   }
   if (t_ana) HIPCHK(hipEventRecord(t_ana, st));
+  if (cj >= 0) p->cnt_sub[cj] = (uint32_t)nf * (uint32_t)p->cmax;
   if (ev_ana) HIPCHK(hipEventRecord(ev_ana, st));  // the norm set is free for execute k+2's norm stage
   // pipelined execute: the frame-size chain (k_frame_scan) only feeds this
   // execute's assembly, so it goes onto the pack stream with it and the plan's stream proceeds straight to
@@ -1099,6 +1148,19 @@ static int run_group(fra_plan* p, const fra_plan::Group& gr, int gi, int ng, hip
   } else {
     HIPCHK(launch_assemble(ga, st));
   }
+  return FRA_OK;
+}
+
+// after an execute: copy its k_analyze_w count (fra_plan::d_cnt17 slot) to page-locked memory on the analysis
+// stream s, behind everything the execute's frame scan, assembly and timing events wait for
+static int count_out(fra_plan* p, hipStream_t s) {
+  const int cj = p->cnt_cur;
+  if (cj < 0) return FRA_OK;
+  p->cnt_cur = -1;
+  HIPCHK(hipMemcpyAsync(p->h_cnt17 + cj, p->d_cnt17 + cj, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(p->ev_cnt[cj], s));
+  p->cnt_pending[cj] = true;
+  p->cnt_seq[cj] = p->cnt_next++;
   return FRA_OK;
 }
 
@@ -1144,6 +1206,7 @@ int fra_plan_execute(fra_plan* p) {
     rc = run_group(p, p->groups[0], 0, 1, as, nullptr, nullptr, nullptr, nullptr, nullptr, -1, nullptr, p->pack,
                    p->ev_scan[b], p->nstream, p->ev_norm[b], p->ev_ana[b]);
     if (rc) return rc;
+    if ((rc = count_out(p, as))) return rc;
     p->ana_pending[b] = true;
     HIPCHK(hipEventRecord(p->ev_nfree[nb], as));  // (the analysis was the last work on `as`)
     p->nfree_pending[nb] = true;
@@ -1164,6 +1227,7 @@ int fra_plan_execute(fra_plan* p) {
       HIPCHK(hipEventRecord(p->ev[4], s));
       p->pending_times = true;
     }
+    if ((rc = count_out(p, s))) return rc;
   } else {
     const int ng = (int)p->groups.size();
     HIPCHK(hipEventRecord(p->gev[0], s));
@@ -1285,7 +1349,9 @@ int fra_plan_flags(fra_plan* p, int32_t* flags) {
   if (!p || !flags) return set_err(FRA_E_INVALID, "null argument");
   // (vector loads as an execute will decide them: the device raster's alignment, or hipMalloc's for host rasters)
   p->args.vec8 = (p->ld_vec8 && (!p->d_raster || (uintptr_t)p->d_raster % 8 == 0)) ? 1 : 0;
-  *flags = (p->pipe ? FRA_PLAN_PIPELINED : 0) | (wave_path(p) ? FRA_PLAN_WAVE : 0);
+  const char* ek = getenv("FRA_KEEP17");
+  const int k17 = (ek && ek[0] == '0') ? 0 : (ek && ek[0] == '1') ? 1 : p->k17;
+  *flags = (p->pipe ? FRA_PLAN_PIPELINED : 0) | (wave_path(p) ? FRA_PLAN_WAVE : 0) | (k17 ? FRA_PLAN_KEEP17 : 0);
   return FRA_OK;
 }
 

@@ -237,6 +237,8 @@ struct JobArgs {
   int32_t frame_count;     //   frames [frame_base, frame_base + frame_count)
   const int32_t* part;     // k_analyze list mode (beside k_analyze_w): (frame * 8 + channel) of the partial
   int32_t npart;           //   subframes of the launch's frames, npart entries (null: the normal grid)
+  uint32_t* cnt17;         // k_analyze_w: += 1 per wave whose kept residuals needed bit 16 (null: not counted)
+  int32_t k17;             // k_analyze_w instance: kept residuals up to 17 bits (1) or 16 (0)
   uint32_t* err;           // plan error word (checked at every sync): bit 0 frame-scan ticket desync, bit 1 a
                            //   frame outside its output / slot bounds (not written)
   const WaveDev* wave;     // [nframes_total]

@@ -387,8 +387,9 @@ class Plan:
         _check(load().fra_plan_set_first_frame(self.h, int(n)))
 
     def flags(self) -> int:
-        """``FRA_PLAN_*`` bits: 2 cross-execute pipelined, 4 full frames on the per-wave analysis kernel (1, direct
-        write, is never set since r03)."""
+        """``FRA_PLAN_*`` bits: 2 cross-execute pipelined, 4 full frames on the per-wave analysis kernel, 8 (with 4)
+        its next execute keeps residuals up to 17 bits (else 16; picked per execute from an earlier one's count of
+        waves that needed bit 16); 1, direct write, is never set since r03."""
         f = C.c_int32()
         _check(load().fra_plan_flags(self.h, C.byref(f)))
         return f.value

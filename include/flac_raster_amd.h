@@ -172,10 +172,14 @@ FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_
  * next execute's normalisation stage and this one's assembly run beside k_analyze); WAVE = full frames are
  * analysed one subframe per wave (k_analyze_w, or k_analyze_w32 when enabled), the partial ones by k_analyze
  * beside it; otherwise every subframe goes to the k_analyze workgroup kernel.  FRA_PLAN_DIRECT_WRITE is never
- * set (the direct-write path was measured slower than slots + k_assemble and removed in r03). */
+ * set (the direct-write path was measured slower than slots + k_assemble and removed in r03).  KEEP17 (with
+ * WAVE) = the next execute's k_analyze_w keeps residuals up to 17 bits (else 16): a pipelined plan picks the
+ * instance from how many waves of an earlier execute needed bit 16 (FRA_KEEP17=0/1 in the environment forces it);
+ * both produce the same bytes. */
 #define FRA_PLAN_DIRECT_WRITE 1
 #define FRA_PLAN_PIPELINED 2
 #define FRA_PLAN_WAVE 4
+#define FRA_PLAN_KEEP17 8
 FRA_API int fra_plan_flags(fra_plan *plan, int32_t *flags);
 
 /* page-locked host memory (hipHostMalloc / hipHostRegister, portable across devices) */

@@ -249,10 +249,12 @@ def test_two_channel_pyflac_path_mid_side():
 
 
 # ---- k_analyze_w (one subframe per wave: full frames of <= 16-bit LUT rasters, levels 3-6, 8-byte sample vectors)
-@pytest.fixture
-def require_wave(monkeypatch):
-    """The plan must take k_analyze_w (FRA_REQUIRE_WAVE=1: the library fails a plan that would not)."""
+@pytest.fixture(params=["1", "0"], ids=["keep17", "keep16"])
+def require_wave(monkeypatch, request):
+    """The plan must take k_analyze_w (FRA_REQUIRE_WAVE=1: the library fails a plan that would not), once with each
+    instance of it (FRA_KEEP17=1: kept residuals up to 17 bits; 0: up to 16, the rest through the sample path)."""
     monkeypatch.setenv("FRA_REQUIRE_WAVE", "1")
+    monkeypatch.setenv("FRA_KEEP17", request.param)
 
 
 @pytest.mark.parametrize("level", [3, 4, 5, 6])
@@ -276,13 +278,16 @@ def test_require_wave_rejects_other_paths(monkeypatch):
         N.encode_windows(r, [(0, 0, 64, 256)], level=8, norm=16)
 
 
+@pytest.mark.parametrize("keep17", ["1", "0"])
 @pytest.mark.parametrize("kind,bands,tile", [(4, 4, 1024), (3, 1, 512)])
-def test_wave_kernel_equals_workgroup_kernel(monkeypatch, kind, bands, tile):
-    """k_analyze_w and k_analyze (FRA_ANALYZE_WG=1) produce the same bytes on a C4-like scene and on a C3-like
-    int16 DEM (whose LPC residuals often pass 2^16: the sample path, codes in the LDS bit buffer)."""
+def test_wave_kernel_equals_workgroup_kernel(monkeypatch, kind, bands, tile, keep17):
+    """k_analyze_w (both instances: kept residuals up to 17 or 16 bits) and k_analyze (FRA_ANALYZE_WG=1) produce the
+    same bytes on a C4-like scene and on a C3-like int16 DEM (whose LPC residuals often pass 2^16: 17-bit kept
+    residuals, or the sample path with codes in the LDS bit buffer)."""
     H = W = 1300
     r = synth_window(kind, 99, bands, H, W)
     wins = tiles(H, W, tile)
+    monkeypatch.setenv("FRA_KEEP17", keep17)
     _, wave = N.encode_windows(r, wins, level=5, norm=16)
     monkeypatch.setenv("FRA_ANALYZE_WG", "1")
     _, wg = N.encode_windows(r, wins, level=5, norm=16)

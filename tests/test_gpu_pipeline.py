@@ -454,3 +454,43 @@ def test_encode_host_pageable_output_worker_counts(threads, monkeypatch):
     finally:
         plan.close()
         ctx.close()
+
+
+@pytest.mark.parametrize("kind,bands,n,tile,want17", [(3, 1, 2048, 512, True), (0, 4, 2100, 1024, False)])
+def test_keep17_instance_follows_the_data(monkeypatch, kind, bands, n, tile, want17):
+    """A pipelined wave-path plan starts on the 17-bit k_analyze_w instance and then takes the one an earlier
+    execute's count of waves that needed bit 16 calls for (FRA_PLAN_KEEP17): the C3-like int16 DEM (a third of its
+    waves) keeps 17 bits, a smooth 4-band ramp with small noise (LPC residuals far below 2^16) drops to 16.  Every
+    execute's bytes are the same whichever instance ran, and equal the oracle's on sampled tiles."""
+    monkeypatch.delenv("FRA_KEEP17", raising=False)
+    if kind:
+        r = synth_window(kind, 7, bands, n, n)
+    else:
+        yy, xx = np.mgrid[0:n, 0:n]
+        noise = np.random.default_rng(3).integers(0, 4, size=(bands, n, n))
+        r = (3 * yy + 2 * xx + 100 * np.arange(bands)[:, None, None] + noise).astype(np.uint16)
+    wins = calculate_tiles(n, n, tile)
+    ctx = N.default_context(0)
+    dev = ctx.alloc(r.nbytes)
+    try:
+        ctx.h2d(dev, r)
+        plan = N.Plan(ctx, dev, True, r.dtype, bands, (n * n, n, 1), wins, 5, 4096, 16)
+        try:
+            assert plan.flags() & 2 and plan.flags() & 4, "needs a pipelined wave-path plan"
+            assert plan.flags() & 8  # no count yet: 17 bits
+            outs = []
+            for _ in range(3):
+                plan.execute()
+                plan.sync()
+                outs.append(plan.download()[1])
+            assert bool(plan.flags() & 8) == want17
+            plan.execute()  # on the chosen instance
+            plan.sync()
+            outs.append(plan.download()[1])
+        finally:
+            plan.close()
+    finally:
+        ctx.free(dev)
+    assert all(o == outs[0] for o in outs[1:])
+    exp = oracle_encode_tiles(r, [wins[0], wins[-1]], level=5)
+    assert bytes(exp[0].body) in outs[-1] and bytes(exp[1].body) in outs[-1]
