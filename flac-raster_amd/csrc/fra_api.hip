@@ -181,8 +181,8 @@ struct fra_plan {
   // while the frame-size chain + assembly of execute k-1 (reading the other set) run on the pack stream
   bool pipe = false;
   int cur = 0;  // buffer set of the last execute
-  // slot sets (descriptors, encoded-subframe slots, frame sizes / offsets): nslot = 2, or 3 (FRA_SLOT_SETS=3: execute
-  // k's analysis then waits for the assembly of execute k-3 instead of k-2); the analysis streams alternate by execute
+  // slot sets (descriptors, encoded-subframe slots, frame sizes / offsets): nslot = 3 (execute k's analysis waits for
+  // the assembly of execute k-3), or 2 when memory is short or FRA_SLOT_SETS=2; the analysis streams alternate by execute
   static constexpr int kSlotSets = 3;
   int nslot = 2;
   unsigned exec_n = 0;
@@ -831,7 +831,10 @@ static int plan_build(fra_plan* p) {
       }
       HIPCHK(hipEventCreateWithFlags(&p->ev_raster, hipEventDisableTiming));
       {
-        static const int want3 = getenv("FRA_SLOT_SETS") ? atoi(getenv("FRA_SLOT_SETS")) : 2;  // A/B
+        // three slot sets by default (r05: with the 16-bit k_analyze_w instance C4 neutral, its 8-way share -4.6 %, C3
+        // -2.3 %, C5 quarter -0.7 %, profiles/r05_ab_background.txt) when twice the extra set fits a third of the free
+        // memory; FRA_SLOT_SETS=2 (A/B) keeps two
+        static const int want3 = getenv("FRA_SLOT_SETS") ? atoi(getenv("FRA_SLOT_SETS")) : 3;
         size_t f2 = 0, t2 = 0;
         p->nslot = (want3 == 3 && hipMemGetInfo(&f2, &t2) == hipSuccess && 2 * extra <= f2 / 3) ? 3 : 2;
       }
