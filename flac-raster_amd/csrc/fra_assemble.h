@@ -58,9 +58,16 @@ __device__ __forceinline__ uint32_t gf16_mul_dev(uint32_t a, uint32_t b) {
   return r & 0xFFFFu;
 }
 
+// FRA_ASM_LIGHT (r05 default): only the Horner level's multiply table in LDS (the per-frame tree's six levels read
+// from the global table, 6 lookups per frame): 9.3 instead of 15.6 KiB per workgroup, so three workgroups fit the
+// 32 KiB a 4-wave k_analyze_w leaves per CU instead of two (with one quad per lane per round, fra_pack.hip)
+#ifndef FRA_ASM_LIGHT
+#define FRA_ASM_LIGHT 1
+#endif
+constexpr int kMLds = FRA_ASM_LIGHT ? 1 : kMLevels;  // LDS multiply tables: levels 10 - kMLds + 1 .. 10
 struct alignas(16) AssembleSmem {
   uint16_t T[16][256];  // slice-by-16: T[k][v] = CRC of v followed by k zero bytes
-  uint16_t M[kMLevels][512];  // multiply by x^(8*2^i), i = 4..10 (tree 4..9, Horner 10)
+  uint16_t M[kMLds][512];  // multiply by x^(8*2^i), i = 4..10 (tree 4..9, Horner 10), or only 10
   uint32_t meta[4][kMetaWords];  // the frame's header words and blob bit bounds (k_frame_scan); [wave]
   uint32_t tailw[4];    // the output window of the last, partial dword (bytes [4*NF - A, L)); [wave]
 };
@@ -78,10 +85,10 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
 // CRC tables to LDS (16-byte loads) so no step of the CRC chain waits on a global gather
 __device__ __forceinline__ void copy_tables(const JobArgs& a, AssembleSmem& S) {
   const uint4* srcT = reinterpret_cast<const uint4*>(a.crctab + kCrcT16Off);
-  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + kMLo * 512);
+  const uint4* srcM = reinterpret_cast<const uint4*>(a.crctab + 1024 + (kMLo + kMLevels - kMLds) * 512);
   uint4* dT = reinterpret_cast<uint4*>(&S.T[0][0]);
   uint4* dM = reinterpret_cast<uint4*>(&S.M[0][0]);
-  constexpr int NTV = 16 * 256 * 2 / 16, NMV = kMLevels * 512 * 2 / 16;  // uint4 counts
+  constexpr int NTV = 16 * 256 * 2 / 16, NMV = kMLds * 512 * 2 / 16;  // uint4 counts
   for (int i = (int)threadIdx.x; i < NTV + NMV; i += kThreads) {
     if (i < NTV) dT[i] = srcT[i];
     else dM[i - NTV] = srcM[i - NTV];
@@ -98,8 +105,9 @@ __device__ __forceinline__ void assemble_frame(const JobArgs& a, const int g, As
   const int t = lane;
   uint32_t* const meta = S.meta[wv];
   uint32_t& tailw = S.tailw[wv];
-  const uint16_t* const M = &S.M[0][0];            // tree levels kMLo..9
-  const uint16_t* const Mh = &S.M[10 - kMLo][0];   // the Horner level: x^(128 NT) = x^(8 * 2^10)
+  // tree levels kMLo..9 (LDS, or the global table: FRA_ASM_LIGHT) and the Horner level x^(128 NT) = x^(8 * 2^10)
+  const uint16_t* const M = FRA_ASM_LIGHT ? a.crctab + 1024 + kMLo * 512 : &S.M[0][0];
+  const uint16_t* const Mh = &S.M[kMLds - 1][0];
   const uint32_t* gmeta = a.fmeta + (size_t)g * kMetaWords;  // uniform
   auto rfl64 = [](uint64_t v) -> uint64_t {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |

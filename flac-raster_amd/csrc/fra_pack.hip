@@ -7,8 +7,12 @@
 #include "fra_assemble.h"
 
 namespace fra {
+// quads per lane per round (r05: 1, 30 VGPRs -- with the lighter LDS tables, FRA_ASM_LIGHT in fra_assemble.h, three
+// workgroups (12 waves) per CU fit beside 4 waves per SIMD of the 16-bit k_analyze_w instead of 8 waves: the assembly of
+// a pipelined execute, which gated the next analysis's start (its slots), keeps up -- C4 step 1.461 -> 1.411 ms, C3 /
+// C5 quarter / 8-way share neutral, profiles/r05_ab_background.txt 10; alone it is 0.282 -> 0.295 ms)
 #ifndef FRA_ASM_U
-#define FRA_ASM_U 2
+#define FRA_ASM_U 1
 #endif
 
 // four frames per workgroup, one per wave -- the 17.5 KiB of CRC tables are copied to LDS
