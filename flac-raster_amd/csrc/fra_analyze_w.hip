@@ -742,10 +742,11 @@ k_analyze_w(JobArgs a, int src) {
       for (int jx = 0; jx < 8; jx++) qm[jx] = __builtin_amdgcn_readlane((int)mv, 8 * wi + jx);
       if (wi == keep_wi) {
         uint32_t um = 0, carry[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll 1
-        for (int j = 0; j < kWIters; j++) {
-          const int t = 64 * j + lane;
-          const bool head = t == 0;
+        // iteration 0 (the only one holding the warm-up samples, lane 0) peeled: the others are compiled with head
+        // false, without the warm-up selects (r05)
+        auto keep_iter = [&](const int j, auto headc) {
+          constexpr bool kHead = decltype(headc)::value;
+          const bool head = kHead && lane == 0;
           uint32_t* const po = sw + 8 * lane + kWIterDw * j;
           uint32_t D[14];
           wread_d14(sw, lane, j, D);
@@ -772,7 +773,10 @@ k_analyze_w(JobArgs a, int src) {
           hk |= (uint64_t)hb << (16 * j);
           const uint64_t gs = bperm64(group_sum_auto(2ull * acc, gsl), psrc);
           psum = pj == j ? gs : psum;
-        }
+        };
+        keep_iter(0, std::true_type{});
+#pragma unroll 1
+        for (int j = 1; j < kWIters; j++) keep_iter(j, std::false_type{});
         const bool need17 = __any(um > 0xFFFFu) && !__any(um > 0x1FFFFu);  // (wave-uniform)
         if (need17 && lane == 0 && a.cnt17) atomicAdd(a.cnt17, 1u);  // (a vector atomic: lane 0 only)
         if constexpr (K17) {
