@@ -177,8 +177,8 @@ struct fra_plan {
   unsigned long long* h_gbase = nullptr;  // page-locked mirror of d_gbase[1..bands]
   unsigned long long* d_gbase_mirror = nullptr;  // its device address
   // cross-execute pipelining (FRA_PIPE, default on when a second buffer set fits in a third of the free
-  // device memory, single frame group): execute k analyses into buffer set k % 2 on the plan's stream
-  // while the frame-size chain + assembly of execute k-1 (reading the other set) run on the pack stream
+  // device memory, single frame group): execute k analyses into slot set k % nslot on an analysis stream
+  // while the frame-size chain + assembly of earlier executes (reading the other sets) run on the pack stream
   bool pipe = false;
   int cur = 0;  // buffer set of the last execute
   // slot sets (descriptors, encoded-subframe slots, frame sizes / offsets): nslot = 3 (execute k's analysis waits for
@@ -192,17 +192,17 @@ struct fra_plan {
   unsigned long long* fbytes2[kSlotSets] = {};
   unsigned long long* foff2[kSlotSets] = {};
   hipStream_t pack = nullptr;
-  // the analysis of buffer set b runs on astream[b] (highest priority): execute k+1's k_analyze is queued
-  // on the other stream than execute k's, so its first workgroups fill the CUs that execute k's tail
-  // leaves idle instead of waiting for that kernel to end
+  // execute k's analysis runs on astream[k % 2] (highest priority): execute k+1's is queued on the other stream
+  // than execute k's, so its first waves fill the CUs that execute k's tail leaves idle instead of waiting for
+  // that kernel to end
   hipStream_t astream[2] = {};
   hipEvent_t ev_scan[kSlotSets] = {}, ev_pack[kSlotSets] = {};
   bool pack_pending[kSlotSets] = {};
   // ... and the normalisation stage (k_minmax -> k_norm_finalize -> k_norm_lut) of execute k+1 runs on
-  // the norm stream under k_analyze of execute k (NormDev/LUT double-buffered with the set).  Neither analysis
-  // leaves room beside it (k_analyze_w: 20 waves x 8 KiB fill the CU's LDS; 32-bps k_analyze: 5 workgroups of
-  // 31.6 KiB), so the background kernels run in the gaps between analysis waves
-  // norm sets (NormDev + table) cycle over kNormSets executes, the slot sets above over 2 (r05): execute k+1's norm
+  // the norm stream under k_analyze of execute k.  k_analyze_w (4 waves of 8 KiB and 97 VGPRs per SIMD) leaves
+  // 32 KiB of LDS and 96 VGPRs per SIMD beside it for the norm stage and the assembly; the 32-bps k_analyze (5
+  // workgroups of 31.6 KiB) leaves none, so there they run in the gaps between analysis waves
+  // norm sets (NormDev + table) cycle over kNormSets executes, the slot sets above over nslot (r05): execute k+1's norm
   // stage waits for execute k-2's analysis, not k-1's, so the norm stream runs up to a whole execute ahead and
   // execute k+1's table is ready before execute k's analysis drains (its waves fill that grid's last, partly empty
   // generation instead of waiting behind a k_minmax_vec that runs ~1.1 ms beside the analysis)

@@ -168,7 +168,7 @@ FRA_API int fra_plan_host_band_rows(fra_plan *plan, int64_t *max_rows);
 FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 /* upper bound of a plan's output bytes (every subframe VERBATIM + headers) and its number of host bands */
 FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
-/* how the plan encodes (FRA_PLAN_*): PIPELINED = executes overlap (double-buffered subframe slots, the
+/* how the plan encodes (FRA_PLAN_*): PIPELINED = executes overlap (two or three sets of subframe slots, the
  * next execute's normalisation stage and this one's assembly run beside k_analyze); WAVE = full frames are
  * analysed one subframe per wave (k_analyze_w, or k_analyze_w32 when enabled), the partial ones by k_analyze
  * beside it; otherwise every subframe goes to the k_analyze workgroup kernel.  FRA_PLAN_DIRECT_WRITE is never
