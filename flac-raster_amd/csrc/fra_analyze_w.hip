@@ -391,7 +391,20 @@ k_analyze_w(JobArgs a, int src) {
   uint32_t* const sw = S.sw;
   const int lane = (int)threadIdx.x;
   FRA_WSTAMP(0)
-  const int g = a.frame_base + (int)blockIdx.x;
+#ifndef FRA_W_XCD
+#define FRA_W_XCD 1
+#endif
+  // XCD-aware frame order (FRA_W_XCD): the dispatcher sends workgroup i (x fastest) to XCD i mod 8, so consecutive
+  // frames -- the same tile's streams and tables -- would spread over all eight L2s; remapped, XCD k takes a
+  // contiguous eighth of each channel's frames (grids of whole multiples of 8 frames; others in order).  r05: step
+  // neutral on C4 / C3, C3's serial analysis -2 % (profiles/r05_ab_xcd_order.txt)
+  int bx = (int)blockIdx.x;
+  if (FRA_W_XCD) {
+    const int nx = (int)gridDim.x, n8 = nx & ~7;
+    const int lin = bx + (int)blockIdx.y * nx;  // dispatch order
+    if ((nx & 7) == 0 && bx < n8) bx = (lin & 7) * (n8 >> 3) + (bx >> 3);
+  }
+  const int g = a.frame_base + bx;
   const int c = (int)blockIdx.y;
   const WaveDev wd = a.wave[g];
   if (c >= wd.nch) return;
