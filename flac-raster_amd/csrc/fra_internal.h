@@ -204,6 +204,11 @@ struct SfDesc {
 constexpr int kCrcT16Off = 1024 + 24 * 512;
 constexpr int kHdrWords = 6;
 constexpr int kMetaWords = 16;
+// wave issue priority (s_setprio) of the background kernels of a pipelined execute -- k_minmax_vec and k_assemble4 --
+// over the co-resident k_analyze_w waves (r05; 0 = off)
+#ifndef FRA_BG_PRIO
+#define FRA_BG_PRIO 2
+#endif
 static_assert(kHdrWords + kMaxChannels + 2 <= kMetaWords, "frame metadata layout");
 
 struct JobArgs {

@@ -124,6 +124,10 @@ __global__ void __launch_bounds__(256) k_minmax_vec(const void* raster, const St
   // vector E-1 (C4: 3,072 slots for 2,048 vectors per band)
   constexpr int U = sizeof(VT) >= 16 ? 4 : 8;
   __shared__ uint32_t smn[4], smx[4];
+  // wave issue priority over co-resident analysis waves (r05: the norm stage of a pipelined execute gates the next
+  // analysis; with it and the assembly at priority 2 -- FRA_BG_PRIO, 0 = off -- C3 -3.6 %, the C4 8-way share -5 %,
+  // C4 and the C5 quarter neutral, profiles/r05_ab_background.txt 14; the analysis raised instead: C4 +5.5 %)
+  if (FRA_BG_PRIO > 0) __builtin_amdgcn_s_setprio(FRA_BG_PRIO);
   const int wv = threadIdx.x >> 6;
   // items (stream, block of `rows` rows) = (item / nrb, item % nrb); a full grid has one item per
   // workgroup (the default, serial and pipelined); a smaller grid (FRA_MM_PER_CU) strides over them

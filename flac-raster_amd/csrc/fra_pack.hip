@@ -21,6 +21,7 @@ namespace fra {
 // per thread per round beat four (`profiles/r03_ab_assemble_per_wave_v20.txt`)
 __global__ void __launch_bounds__(kThreads, 8) k_assemble4(JobArgs a) {
   __shared__ AssembleSmem S;
+  if (FRA_BG_PRIO > 0) __builtin_amdgcn_s_setprio(FRA_BG_PRIO);  // (wave issue priority: fra_internal.h)
   copy_tables(a, S);
   __syncthreads();
   const int i = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
