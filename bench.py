@@ -8,10 +8,11 @@ A *step* = one pass of the encode hot path over the whole scene: device-resident
 per-tile nanmin/nanmax -> normalize_to_audio -> FLAC analysis -> bit-packed frames of every tile
 in HBM (the bytes the reference's pyflac/libFLAC calls produce per tile, cli.py:553-622).
 
-Multi-GPU (one process per GPU, torch.distributed.run): STRONG scaling by default -- BASELINE's C4/C5
-are ONE scene whose tiles are sharded over the GPUs (LPT on pixel count), no collective
-on the data path; ``value`` = scene pixels / max-over-ranks time; per-rank times and the imbalance are
-reported.  ``--scaling weak`` instead gives every rank its own scene (seed + rank).
+Multi-GPU (one process per GPU): under torch.distributed.run, or ``--gpus N`` alone, which starts the N rank
+processes itself before touching the GPU.  STRONG scaling by default -- BASELINE's C4/C5 are ONE scene split
+over the GPUs into (tile, frame range) items of equal frame count (``--split frames``), no
+collective on the data path; ``value`` = scene pixels / max-over-ranks time; per-rank times and the imbalance
+are reported.  ``--scaling weak`` instead gives every rank its own scene (seed + rank).
 
 Also reported (rank 0):
 * ``roofline`` of the dominant kernel: HIP events on the plan's stream; algorithmic bytes = input raster
@@ -379,10 +380,77 @@ def committed_profile(args, cfg, kernel):
     return out
 
 
+# ------------------------------------------------------------------------------------- rank launcher
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus():
+    """GPUs this process may use, counted WITHOUT initialising HIP (torch.cuda.device_count() reads the
+    KFD topology on this image; no HIP call), so the launcher can still start fresh rank processes."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` without a launcher (no WORLD_SIZE): start N fresh rank processes of this script,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1), before this process touches the
+    GPU; relay rank 0's JSON line and fail if any rank fails.  More ranks than visible GPUs is refused unless
+    FRA_DIST_BACKEND=gloo asks for a rehearsal (ranks share GPUs; the line is labelled ``rehearsal``)."""
+    ndev = visible_gpus()
+    env0 = dict(os.environ)
+    if n > ndev:
+        if env0.get("FRA_DIST_BACKEND") != "gloo" or ndev < 1:
+            raise SystemExit(f"bench.py --gpus {n}: only {ndev} GPU(s) visible (set FRA_DIST_BACKEND=gloo to "
+                             f"rehearse {n} ranks on fewer GPUs)")
+    port = _free_port()
+    outs, procs = [], []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FRA_BENCH_LAUNCHED="1")
+        out = tempfile.TemporaryFile(mode="w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env,
+                                      stdout=out, stderr=None))
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad
+            for p in procs:  # our own children, by PID: a rank that died leaves the others at a barrier
+                if p.poll() is None:
+                    p.terminate()
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.2)
+    for r, out in enumerate(outs):
+        out.seek(0)
+        text = out.read()
+        out.close()
+        if r == 0:
+            sys.stdout.write(text)
+            sys.stdout.flush()
+        elif text.strip():
+            sys.stderr.write(f"[rank {r}] {text}")
+    if failed is not None:
+        raise SystemExit(f"bench.py --gpus {n}: rank(s) failed: " +
+                         ", ".join(f"rank {r} exit {c}" for r, c in failed))
+
+
 # ------------------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank process each); without a launcher N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
@@ -391,7 +459,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
     ap.add_argument("--shard", default=None, metavar="R/N",
-                    help="time rank R's LPT share of the scene for an N-GPU strong-scaling run, on this one GPU "
+                    help="time rank R's share (--split) of the scene for an N-GPU strong-scaling run, on this one GPU "
                          "(projection of the multi-GPU step; DESIGN.md section 7)")
     ap.add_argument("--split", default="frames", choices=["frames", "strided", "lpt"],
                     help="strong scaling: (tile, frame range) work items of equal frame count per rank (default; "
@@ -412,15 +480,29 @@ def main():
     if args.level is not None:
         cfg["level"] = args.level
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1 and not (args.child or args.shard):
+            launch_ranks(args.gpus, sys.argv[1:])  # N fresh rank processes; this one never touches the GPU
+            return
+        if args.gpus is not None and args.gpus < 1:
+            raise SystemExit("--gpus must be >= 1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={world}")
+    rehearsal = None
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist_mod
         # RCCL over xGMI on a GPU node; FRA_DIST_BACKEND=gloo rehearses several ranks on one GPU
         backend = os.environ.get("FRA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        ndev = torch.cuda.device_count()
+        if world > ndev:
+            if backend != "gloo":
+                raise SystemExit(f"{world} ranks but {ndev} GPU(s): FRA_DIST_BACKEND=gloo rehearses ranks sharing GPUs")
+            rehearsal = f"{world} ranks on {ndev} GPU(s)"
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist_mod.init_process_group(backend=backend)
@@ -488,20 +570,46 @@ def main():
         ctx.free(dev_raster)
         return
 
-    plan.execute()  # (untimed: settles the k_analyze_w instance, FRA_PLAN_KEEP17, even at --warmup 0)
+    # (untimed: settles the k_analyze_w instance, FRA_PLAN_KEEP17, even at --warmup 0).  A plan's first execute
+    # has no count yet and runs the 17-bit instance: its synced time is reported as first_execute_ms (cold: it
+    # also pays the first launch of every kernel)
+    t0 = time.perf_counter()
+    plan.execute()
     plan.sync()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    first_inst = (17 if plan.flags() & 8 else 16) if wave_plan else None
     for _ in range(args.warmup):
         plan.execute()
     plan.sync()
     barrier()
     plan.sync()
+    inst = []  # the k_analyze_w instance each timed execute ran (flags() & 8 right after it: the one it launched)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         plan.execute()
+        inst.append(plan.flags() & 8)
     plan.sync()
     t1 = time.perf_counter()
     barrier()
     dt_s = t1 - t0
+    inst = [17 if f else 16 for f in inst] if wave_plan else None
+    # the same pipelined steps forced onto the 17-bit instance (what a plan runs before its count arrives, and on
+    # data where more than 1/32 of the waves need bit 16): the adaptive pick's worth, reported beside ms_per_step
+    k17_ms = None
+    if wave_plan and os.environ.get("FRA_KEEP17") is None:
+        os.environ["FRA_KEEP17"] = "1"  # read by every execute (getenv)
+        try:
+            plan.execute()
+            plan.sync()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                plan.execute()
+            plan.sync()
+            k17_ms = (time.perf_counter() - t0) / args.steps * 1e3
+            barrier()
+        finally:
+            del os.environ["FRA_KEEP17"]
     # per-kernel launch times (roofline): the same steps again, serial, HIP events between kernels
     plan.enable_timing(True)
     for _ in range(args.steps):
@@ -642,13 +750,15 @@ def main():
             valu_frac = pm["valu_insts"] * VALU_CYC / (SIMDS * pm["busy_cycles_per_xcd"])
         bound = "hbm" if valu_frac is None or hbm_frac >= valu_frac else "valu"
         per_rank = [{"rank": k, "ms_per_step": round(r[0] / args.steps * 1e3, 4), "analyze_ms": round(r[1], 4),
-                     "serial_ms": round(r[2], 4), "tiles": int(r[3]), "pixels": int(r[4])} for k, r in enumerate(ranks)]
+                     "serial_ms": round(r[2], 4), "tiles": int(r[3]), "pixels": int(r[4]),
+                     "frame_bytes": int(r[5])} for k, r in enumerate(ranks)]
         mean_t = sum(r[0] for r in ranks) / len(ranks)
         result = {
             "metric": "raster MPixels/sec encoded at -c 5 + size ratio vs libFLAC, 1/2/4/8 GPU",
             "value": round(value, 2),
             "unit": "MPix/s",
             "n_gpus": world,
+            **({"rehearsal": rehearsal} if rehearsal else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(T / args.steps * 1e3, 4),
@@ -662,10 +772,24 @@ def main():
                        "compression_ratio": round(raster_bytes * (world if weak else 1) / max(1.0, out_bytes_all), 4),
                        "msamples_per_s": round(job_px * B * args.steps / T / 1e6, 1),
                        "parallelism": (f"{world} scene(s), one per GPU, no collective" if weak else
-                                       f"one scene's tiles sharded LPT over {world} GPU(s), no collective"),
+                                       "one scene over {} GPU(s), no collective: {}".format(world, {
+                                           "frames": "(tile, frame range) items of equal frame count per rank",
+                                           "strided": "(tile, frame range) items of equal frame count per rank, "
+                                                      "tiles in strided order",
+                                           "lpt": "whole tiles by LPT on pixel count"}[args.split])),
+                       "split": args.split,
                        "serial_ms_per_step": round(step_ms_local, 4)},
             "per_rank": per_rank,
             "imbalance": round(T / mean_t, 4) if mean_t > 0 else None,
+            "analysis_instance": ({
+                "timed_executes": {str(b): inst.count(b) for b in sorted(set(inst))},
+                "first_execute": first_inst, "first_execute_ms": round(first_ms, 4),
+                "ms_per_step_forced_17bit": round(k17_ms, 4) if k17_ms is not None else None,
+                "note": "k_analyze_w keeps residuals up to 17 or 16 bits; a plan picks per execute from an earlier "
+                        "execute's count of waves that needed bit 16 (FRA_PLAN_KEEP17). The timed executes re-encode "
+                        "the same scene, so they run the instance the settle execute's count chose; bytes are equal "
+                        "either way. first_execute_ms is the plan's first (17-bit, cold) execute, synced alone"}
+                if inst is not None else None),
             "roofline": {"bound": bound, "kernel": dom_label, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(hbm_frac, 5), "traffic": pm.get("traffic"),
                          "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,

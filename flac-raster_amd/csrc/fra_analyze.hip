@@ -1367,7 +1367,6 @@ namespace fra {
 #endif
 
 hipError_t launch_analyze_w(int src, int level, const JobArgs& a, int cw, hipStream_t s);
-hipError_t launch_analyze_w32(int src, int level, const JobArgs& a, int cw, hipStream_t s);
 
 // wave: 16-bit plans whose full frames k_analyze_w takes (fra_api.hip wave_path): k_analyze_w over the launch's
 // frames, k_analyze over `part` (the launch's npart partial subframes, frame * 8 + channel), both complete
@@ -1394,15 +1393,14 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
   dim3 grid((unsigned)a.frame_count, (unsigned)a.cmax);
   const LevelCfg cfg = level_cfg(a.level);
   const int ml = cfg.nsub == 0 ? 0 : (cfg.max_lpc <= 8 ? 8 : 12);
-  if (wave && ((!b32 && ml == 8) || (b32 && !ms && ml == 12))) {
+  if (wave && !b32 && ml == 8) {
     const int cw = ms ? 2 : a.cmax;
     hipError_t e = hipSuccess;
     auto partial = [&](hipStream_t ps) {
       JobArgs wa = a;
       wa.part = part;
       wa.npart = npart;
-      if (b32) k_analyze<true, 12><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
-      else k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);
+      k_analyze<false, 8><<<(unsigned)npart, kThreads, 0, ps>>>(wa, src);  // one workgroup per entry
     };
     const bool fork = npart > 0 && side;
     if (fork) {
@@ -1411,8 +1409,7 @@ hipError_t launch_analyze(int src, bool b32, bool ms, const JobArgs& a, hipStrea
       partial(side);
       if ((e = hipEventRecord(ev_join, side)) != hipSuccess) return e;
     }
-    if ((e = b32 ? launch_analyze_w32(src, a.level, a, cw, s) : launch_analyze_w(src, a.level, a, cw, s)) != hipSuccess)
-      return e;
+    if ((e = launch_analyze_w(src, a.level, a, cw, s)) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return e;
     if (npart > 0 && !side) partial(s);
     if (ms) {

@@ -734,7 +734,7 @@ static int plan_build(fra_plan* p) {
     if (j.blocksize == kMaxBlock && ((!p->b32 && j.level >= 3 && j.level <= 6 && j.norm != 0 &&
                                       elem_size(j.dtype) <= 2 && j.dtype != FRA_F64) ||
                                      (p->b32 && j.level >= 7 && j.norm == 24 && j.dtype == FRA_F32 &&
-                                      j.channels == p->cmax))) {  // plans k_analyze_w / k_analyze_w32 may take (wave_path)
+                                      j.channels == p->cmax))) {  // plans k_analyze_w may take (wave_path)
       // the partial subframes (frame * 8 + channel, ascending): k_analyze's share of a wave-path launch
       p->h_part.clear();
       for (int g = 0; g < nfr; g++) {
@@ -910,14 +910,11 @@ static int drain_pipeline(fra_plan* p) {
   use_buffers(p, 0, 0);
   return FRA_OK;
 }
-static int plan_sync_all(fra_plan* p) {
-  for (auto& st : p->astream)
-    if (st) HIPCHK(hipStreamSynchronize(st));
-  if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
-  if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
-  HIPCHK(hipStreamSynchronize(p->ctx->stream));
-  // device-detected inconsistencies (JobArgs::err): bit 0 a frame-scan ticket past its grid, bit 1 a frame the
-  // assembly did not write because its sizes left the output or its slots -- the stream is not handed back
+// device-detected inconsistencies (JobArgs::err): bit 0 a frame-scan ticket past its grid, bit 1 a frame the
+// assembly did not write because its sizes left the output or its slots -- the stream is not handed back.  The
+// word is sticky: once set, every later sync / result / host encode of the plan reports it (call after the work
+// that may set it has completed)
+static int check_dev_err(fra_plan* p) {
   if (p->d_err) {
     uint32_t e = 0;
     HIPCHK(hipMemcpy(&e, p->d_err, sizeof(e), hipMemcpyDeviceToHost));
@@ -925,6 +922,14 @@ static int plan_sync_all(fra_plan* p) {
                           (e & 2u) ? "frame outside its output/slot bounds" : "");
   }
   return FRA_OK;
+}
+static int plan_sync_all(fra_plan* p) {
+  for (auto& st : p->astream)
+    if (st) HIPCHK(hipStreamSynchronize(st));
+  if (p->nstream) HIPCHK(hipStreamSynchronize(p->nstream));
+  if (p->pack) HIPCHK(hipStreamSynchronize(p->pack));
+  HIPCHK(hipStreamSynchronize(p->ctx->stream));
+  return check_dev_err(p);
 }
 
 int fra_plan_set_raster(fra_plan* p, const void* raster, int32_t on_device) {
@@ -987,11 +992,18 @@ static int plan_create(fra_ctx* ctx, const fra_job* job, const int32_t* franges,
   p->windows.assign(job->windows, job->windows + job->nwindows);
   p->job.windows = p->windows.data();
   if (franges) {
-    for (int w = 0; w < job->nwindows; w++)
-      if (franges[2 * w] < 0) {
+    // a range must lie inside its window's stream: a first frame past the end or a negative count other than
+    // -1 (to the end) would silently drop or duplicate frames of a multi-GPU work split
+    for (int w = 0; w < job->nwindows; w++) {
+      const fra_window& wd = job->windows[w];
+      const int64_t nfr_all = ((int64_t)wd.width * wd.height + job->blocksize - 1) / job->blocksize;
+      const int32_t f0 = franges[2 * w], n = franges[2 * w + 1];
+      if (f0 < 0 || f0 > nfr_all || n < -1 || (n >= 0 && (int64_t)f0 + n > nfr_all)) {
         delete p;
-        return set_err(FRA_E_INVALID, "window %d: first frame %d < 0", w, franges[2 * w]);
+        return set_err(FRA_E_INVALID, "window %d: frame range (%d, %d) outside its %lld frames", w, f0, n,
+                       (long long)nfr_all);
       }
+    }
     p->franges.assign(franges, franges + 2 * (size_t)job->nwindows);
   }
   int rc = plan_build(p);
@@ -1023,13 +1035,9 @@ static void collect_times(fra_plan* p) {
 static bool wave_path(const fra_plan* p) {
   const bool wg = getenv("FRA_ANALYZE_WG") && atoi(getenv("FRA_ANALYZE_WG")) == 1;
   if (wg || !p->wave_ok || !p->args.vec8 || !p->args.off32 || p->job.blocksize != kMaxBlock) return false;
-  if (p->b32) {  // k_analyze_w32 (r05, opt-in FRA_W32=1): float32 rasters normalised to 24 bits, levels 7-8.
-    // Bytes identical to k_analyze<true, 12>, but measured slower (C5 quarter 28.5 against 22.8 ms of analysis,
-    // profiles/r05_ab_w32_c5q.txt): at 16 KiB of LDS per wave only 2 waves per SIMD run, each re-reads and
-    // re-converts its samples per model (the workgroup kernel holds one chunk per thread across all models)
-    const bool w32 = getenv("FRA_W32") && atoi(getenv("FRA_W32")) == 1;
-    return w32 && p->job.norm == 24 && p->job.dtype == FRA_F32 && p->job.level >= 7 && p->job.level <= 8;
-  }
+  // (32-bps plans stay on k_analyze: a one-subframe-per-wave 32-bps kernel, r05's k_analyze_w32, was measured
+  // slower -- C5 quarter 28.5 against 22.8 ms of analysis, profiles/r05_ab_w32_c5q.txt -- and removed in r06)
+  if (p->b32) return false;
   return p->args.lut && p->job.level >= 3 && p->job.level <= 6;  // k_analyze_w
 }
 // one frame group on stream st: minmax/LUT of its windows, analysis, frame sizes, the group's own scan,
@@ -1608,15 +1616,26 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
   std::unique_lock<std::mutex> stage_lk(cx->stage_mu, std::defer_lock);
   const bool out_pageable = capacity > 0 && !host_pinned(host_out) && stage_lk.try_lock();
   if (out_pageable && !cx->stage) {
+    // built in locals and committed to the context only when every piece exists (a half-built staging
+    // set would leave a worker pool with no threads that reports success without copying)
     const char* e = getenv("FRA_D2H_THREADS");
     const int n = std::min(std::max(e ? atoi(e) : 4, 1), 16);
-    HIPCHK(hipHostMalloc((void**)&cx->stage, D2HWorker::kPiece * n, hipHostMallocPortable));
-    cx->stage_n = n;
-    for (int i = 0; i < n; i++) {
+    uint8_t* stage = nullptr;
+    std::vector<hipStream_t> sts;
+    hipError_t he = hipHostMalloc((void**)&stage, D2HWorker::kPiece * n, hipHostMallocPortable);
+    for (int i = 0; he == hipSuccess && i < n; i++) {
       hipStream_t st = nullptr;
-      HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-      cx->stage_st.push_back(st);
+      he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+      if (he == hipSuccess) sts.push_back(st);
     }
+    if (he != hipSuccess) {
+      for (auto st : sts) (void)hipStreamDestroy(st);
+      if (stage) (void)hipHostFree(stage);
+      return set_err(FRA_E_HIP, "D2H staging: %s", hipGetErrorString(he));
+    }
+    cx->stage = stage;
+    cx->stage_n = n;
+    cx->stage_st = std::move(sts);
   }
   D2HWorker dw(cx->device, out_pageable ? host_out : nullptr, p->d_out, cx->stage, cx->stage_st);
   auto enqueue_d2h = [&](int b) -> int {
@@ -1644,37 +1663,48 @@ static int encode_host(fra_plan* p, const void* host_raster, uint8_t* host_out, 
     g_err = keep;
     return code;
   };
+  // (a HIP error once copies are in flight also drains: the caller may free or refill its ring on return)
+#define HIPCHK_D(x)                                                                                         \
+  do {                                                                                                      \
+    hipError_t _e = (x);                                                                                    \
+    if (_e != hipSuccess)                                                                                   \
+      return drained(set_err(FRA_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(_e), __FILE__, __LINE__)); \
+  } while (0)
   int rc = enqueue_copy(0);
   if (rc) return drained(rc);
   for (int b = 0; b < nb; b++) {
     if (b + 1 < nb) {  // the next band's rows go over PCIe meanwhile
       while (ahead > 0 && b + 1 - issued > ahead) {
-        HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
+        HIPCHK_D(hipEventSynchronize(p->hev[2 * issued + 1]));
         if ((rc = enqueue_d2h(issued++))) return drained(rc);
       }
       if ((rc = enqueue_copy(b + 1))) return drained(rc);
     }
-    HIPCHK(hipStreamWaitEvent(s, p->hev[2 * b], 0));
+    HIPCHK_D(hipStreamWaitEvent(s, p->hev[2 * b], 0));
     // the band's end offset reaches h_gbase by a kernel store (k_group_offsets), not by a copy-engine
     // command that would queue behind the H2D copies
     rc = run_group(p, p->hbands[b].g, b, nb, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p->d_gbase_mirror);
     if (rc) return drained(rc);
-    HIPCHK(hipEventRecord(p->hev[2 * b + 1], s));
+    HIPCHK_D(hipEventRecord(p->hev[2 * b + 1], s));
     // bands already assembled: their D2H can start now (pageable sources make the H2D enqueue blocking)
     while (issued <= b && hipEventQuery(p->hev[2 * issued + 1]) == hipSuccess)
       if ((rc = enqueue_d2h(issued++))) return drained(rc);
     publish();
   }
   while (issued < nb) {
-    HIPCHK(hipEventSynchronize(p->hev[2 * issued + 1]));
+    HIPCHK_D(hipEventSynchronize(p->hev[2 * issued + 1]));
     if ((rc = enqueue_d2h(issued++))) return drained(rc);
   }
   if (!dw.finish()) return drained(set_err(FRA_E_HIP, "frames D2H: %s", dw.error().c_str()));
-  HIPCHK(hipStreamSynchronize(p->d2h));
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipStreamSynchronize(p->h2d));
+  HIPCHK_D(hipStreamSynchronize(p->d2h));
+  HIPCHK_D(hipStreamSynchronize(s));
+  HIPCHK_D(hipStreamSynchronize(p->h2d));
+#undef HIPCHK_D
   publish();
   p->executed = true;
+  // a frame the assembly skipped or a frame-scan desync (the device error word) fails the call: the copied
+  // frames are not a valid stream
+  if ((rc = check_dev_err(p))) return rc;
   if (total_bytes) *total_bytes = beg;
   if (over)
     return set_err(FRA_E_SPACE, "output needs %llu bytes, capacity %llu (frames stay on the device)",

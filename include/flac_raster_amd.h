@@ -110,7 +110,8 @@ FRA_API int fra_plan_create(fra_ctx *ctx, const fra_job *job, fra_plan **out);
  * w.  The normalisation (data_min/max, sample rate) still spans the whole window and the frames keep their
  * frame numbers, so the concatenated frames of all ranges of one window, in order, are exactly the stream
  * fra_plan_create would encode (the reference encodes a window as one stream, cli.py:553-597).
- * fra_stream_info.nframes / frame_bytes describe the range. */
+ * fra_stream_info.nframes / frame_bytes describe the range.  A range outside the window's stream (first frame
+ * < 0 or past its frame count, count < -1 or past the end) is FRA_E_INVALID. */
 FRA_API int fra_plan_create_ranged(fra_ctx *ctx, const fra_job *job, const int32_t *frame_ranges, fra_plan **out);
 FRA_API int fra_plan_set_raster(fra_plan *plan, const void *raster, int32_t raster_on_device);
 FRA_API int fra_plan_execute(fra_plan *plan);
@@ -170,7 +171,7 @@ FRA_API int fra_plan_set_first_frame(fra_plan *plan, int32_t first_frame);
 FRA_API int fra_plan_capacity(fra_plan *plan, uint64_t *capacity, int32_t *host_bands);
 /* how the plan encodes (FRA_PLAN_*): PIPELINED = executes overlap (two or three sets of subframe slots, the
  * next execute's normalisation stage and this one's assembly run beside k_analyze); WAVE = full frames are
- * analysed one subframe per wave (k_analyze_w, or k_analyze_w32 when enabled), the partial ones by k_analyze
+ * analysed one subframe per wave (k_analyze_w), the partial ones by k_analyze
  * beside it; otherwise every subframe goes to the k_analyze workgroup kernel.  FRA_PLAN_DIRECT_WRITE is never
  * set (the direct-write path was measured slower than slots + k_assemble and removed in r03).  KEEP17 (with
  * WAVE) = the next execute's k_analyze_w keeps residuals up to 17 bits (else 16): a pipelined plan picks the

@@ -55,3 +55,41 @@ def test_distributed_gpu_container_equals_single_process(tmp_path, world, dtype,
     single = tmp_path / "single.flac"
     create_streaming_flac(src, single, tile, level)
     assert out.read_bytes() == single.read_bytes()
+
+
+def _bench_line(args, env_extra, timeout=240):
+    import json
+    import os
+    env = dict(os.environ, **env_extra)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(HERE.parent / "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_bench_gpus_flag_starts_the_ranks_itself():
+    """``bench.py --gpus 2`` without a launcher starts two fresh rank processes (here both on
+    device 0 over gloo, a labelled rehearsal) and reports a 2-GPU line whose frames equal the 1-rank line's
+    (reference loop being sharded: cli.py:553-622)."""
+    common = ["--config", "c3", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-pmc", "--no-trace"]
+    one = _bench_line(["--gpus", "1", *common], {})
+    two = _bench_line(["--gpus", "2", *common], {"FRA_DIST_BACKEND": "gloo"})
+    assert one["n_gpus"] == 1 and "rehearsal" not in one
+    assert two["n_gpus"] == 2 and two["rehearsal"].startswith("2 ranks on")
+    assert len(two["per_rank"]) == 2 and all(r["frame_bytes"] > 0 for r in two["per_rank"])
+    assert two["config"]["compressed_bytes"] == one["config"]["compressed_bytes"]
+    assert sum(r["frame_bytes"] for r in two["per_rank"]) == one["config"]["compressed_bytes"]
+    assert two["config"]["split"] == "frames" and "frame range" in two["config"]["parallelism"]
+    assert one["analysis_instance"]["first_execute"] == 17
+
+
+def test_bench_gpus_flag_refuses_more_ranks_than_gpus():
+    import os
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "FRA_DIST_BACKEND"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(HERE.parent / "bench.py"), "--gpus", "64", "--config", "c3"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr

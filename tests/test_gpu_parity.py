@@ -336,38 +336,18 @@ def test_wave_kernel_large_rice_parameters(require_wave, amp):
     check_windows(r, [(0, 0, 128, 512), (0, 0, 64, 256)], 5, 16)
 
 
-# ---- k_analyze_w32 (r05: one 32-bps subframe per wave: float32 rasters normalised to 24 bits, levels 7-8; opt-in
-# FRA_W32=1 -- measured slower than the workgroup kernel, DESIGN.md 5.0b -- and held to the same bytes)
-@pytest.fixture
-def w32(monkeypatch):
-    monkeypatch.setenv("FRA_W32", "1")
-
-
+# ---- 32-bps full + partial frames at levels 7-8 (k_analyze<true, 12>; r05's opt-in one-wave k_analyze_w32, which
+# these cases pinned, lost to it and was removed in r06)
 @pytest.mark.parametrize("level", [7, 8])
-def test_wave32_kernel_levels(w32, require_wave, level):
-    """Both levels the 32-bps wave kernel takes (3 / 6 apodization windows, lag 12), full + partial frames (partial
-    ones through k_analyze's list) against the oracle."""
+def test_32bps_levels_full_and_partial_frames(level):
+    """Both high levels of the 32-bps path (3 / 6 apodization windows, lag 12), full and partial frames."""
     r = synth_window(5, 9 + level, 3, 300, 704).astype(np.float32)
     check_windows(r, [(0, 0, 300, 704), (0, 0, 64, 64), (17, 8, 131, 256)], level, 24)
 
 
-def test_wave32_equals_workgroup_kernel(w32, monkeypatch):
-    """k_analyze_w32 and k_analyze<true, 12> (FRA_ANALYZE_WG=1) produce the same bytes on a C5-like scene."""
-    H = W = 1300
-    r = synth_window(5, 99, 4, H, W).astype(np.float32)
-    wins = tiles(H, W, 512)
-    monkeypatch.setenv("FRA_REQUIRE_WAVE", "1")
-    _, wave = N.encode_windows(r, wins, level=8, norm=24)
-    monkeypatch.delenv("FRA_REQUIRE_WAVE")
-    monkeypatch.setenv("FRA_ANALYZE_WG", "1")
-    _, wg = N.encode_windows(r, wins, level=8, norm=24)
-    assert wave == wg
-
-
-def test_wave32_noise_constant_and_overrun(w32, require_wave):
-    """Full-range noise bands (VERBATIM: the samples loaded again after the residual pass overwrote them), constant
-    frames, and frames whose first quarter is noise before a smooth rest (the encoded bits overrun the residuals
-    in LDS: codes ORed straight into the slot)."""
+def test_32bps_noise_constant_and_overrun():
+    """Full-range noise bands (VERBATIM), constant frames, and frames whose first quarter is noise before a smooth
+    rest (encoded bits overrun the samples they alias)."""
     rng = np.random.default_rng(31)
     r = synth_window(5, 5, 3, 256, 512).astype(np.float32)
     r[1] = rng.standard_normal(r[1].shape).astype(np.float32)

@@ -406,6 +406,21 @@ def test_ranged_plan_frames_equal_stream_slices(kind, dtype, level, norm):
         base += nfr[k]
 
 
+def test_ranged_plan_rejects_ranges_outside_the_stream():
+    """a (tile, frame range) work item outside its window's stream -- a first frame past the stream's
+    frame count, a count below -1 or past the end -- is rejected at plan creation instead of silently dropping or
+    duplicating frames of the multi-GPU split."""
+    ctx = N.default_context(0)
+    wins = calculate_tiles(512, 512, 256)  # 16 frames per window
+    ok = [(0, -1), (15, 1), (16, 0), (3, 13)]
+    plan = N.Plan(ctx, None, False, np.uint16, 1, (512 * 512, 512, 1), wins, 5, 4096, 16, frame_ranges=ok)
+    plan.close()
+    for bad in [(17, -1), (0, -5), (10, 7), (-1, 2)]:
+        with pytest.raises(N.NativeError, match="frame range|first frame"):
+            N.Plan(ctx, None, False, np.uint16, 1, (512 * 512, 512, 1), wins, 5, 4096, 16,
+                   frame_ranges=[bad] + ok[1:])
+
+
 def test_plan_rejects_bad_strides():
     """Strides are validated at plan creation (negative strides, col_stride < 1, row_stride >= 2^32 elements:
     the per-frame analysis descriptors hold the row stride in 32 bits)."""
@@ -494,3 +509,35 @@ def test_keep17_instance_follows_the_data(monkeypatch, kind, bands, n, tile, wan
     assert all(o == outs[0] for o in outs[1:])
     exp = oracle_encode_tiles(r, [wins[0], wins[-1]], level=5)
     assert bytes(exp[0].body) in outs[-1] and bytes(exp[1].body) in outs[-1]
+
+
+def test_keep17_instance_on_a_subset_of_the_c4_bench_scene(monkeypatch):
+    """the bench's C4 scene settles on the 16-bit k_analyze_w instance; a plan over a subset of
+    that same scene's 1024^2 tiles (tile rows 4-5, 22 tiles incl. two 740-wide edge tiles, generated on the device
+    exactly as bench.py does) must settle on it too, so the instance the bench line reports is not a property of
+    re-encoding the whole scene only.  Bytes are the same on either instance."""
+    monkeypatch.delenv("FRA_KEEP17", raising=False)
+    H = W = 10980
+    ctx = N.default_context(0)
+    dev = ctx.alloc(4 * H * W * 2)
+    try:
+        ctx.synth(4, 20260227, 4, H, W, dev)
+        wins = [w for w in calculate_tiles(H, W, 1024) if w[0] in (4096, 5120)]
+        assert len(wins) == 22
+        plan = N.Plan(ctx, dev, True, np.uint16, 4, (H * W, W, 1), wins, 5, 4096, 16)
+        try:
+            assert plan.flags() & 2 and plan.flags() & 4 and plan.flags() & 8
+            outs = []
+            for _ in range(3):
+                plan.execute()
+                plan.sync()
+                outs.append(plan.download()[1])
+            assert not plan.flags() & 8, "the C4 subset stayed on the 17-bit instance"
+            plan.execute()
+            plan.sync()
+            outs.append(plan.download()[1])
+        finally:
+            plan.close()
+    finally:
+        ctx.free(dev)
+    assert all(o == outs[0] for o in outs[1:])

@@ -387,3 +387,21 @@ def test_audio_params_host(golden_dir):
         assert normalization.calculate_audio_params(S, row["dtype"]) == (row["sample_rate"], row["bps"])
     assert normalization.get_dtype_info(np.uint16) == (0.0, 65535.0, True)
     assert normalization.get_dtype_info(np.float32) == (None, None, False)
+
+
+def test_bench_gpus_flag_fails_loudly_without_enough_gpus():
+    """``bench.py --gpus N`` starts its own ranks only onto visible GPUs: with none here it must
+    exit non-zero before any rank starts, instead of timing one process and printing an ``n_gpus: 1`` line."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "FRA_DIST_BACKEND"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "c3"], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr and not r.stdout.strip()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--config", "c3"], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
