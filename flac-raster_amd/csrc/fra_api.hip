@@ -992,13 +992,14 @@ static int plan_create(fra_ctx* ctx, const fra_job* job, const int32_t* franges,
   p->windows.assign(job->windows, job->windows + job->nwindows);
   p->job.windows = p->windows.data();
   if (franges) {
-    // a range must lie inside its window's stream: a first frame past the end or a negative count other than
-    // -1 (to the end) would silently drop or duplicate frames of a multi-GPU work split
+    // a range must start inside its window's stream (a count past the end is clipped to it): a first frame past
+    // the end or a negative count other than -1 (to the end) is a malformed work item of a multi-GPU split
+    // 
     for (int w = 0; w < job->nwindows; w++) {
       const fra_window& wd = job->windows[w];
       const int64_t nfr_all = ((int64_t)wd.width * wd.height + job->blocksize - 1) / job->blocksize;
       const int32_t f0 = franges[2 * w], n = franges[2 * w + 1];
-      if (f0 < 0 || f0 > nfr_all || n < -1 || (n >= 0 && (int64_t)f0 + n > nfr_all)) {
+      if (f0 < 0 || f0 > nfr_all || n < -1) {
         delete p;
         return set_err(FRA_E_INVALID, "window %d: frame range (%d, %d) outside its %lld frames", w, f0, n,
                        (long long)nfr_all);

@@ -110,8 +110,8 @@ FRA_API int fra_plan_create(fra_ctx *ctx, const fra_job *job, fra_plan **out);
  * w.  The normalisation (data_min/max, sample rate) still spans the whole window and the frames keep their
  * frame numbers, so the concatenated frames of all ranges of one window, in order, are exactly the stream
  * fra_plan_create would encode (the reference encodes a window as one stream, cli.py:553-597).
- * fra_stream_info.nframes / frame_bytes describe the range.  A range outside the window's stream (first frame
- * < 0 or past its frame count, count < -1 or past the end) is FRA_E_INVALID. */
+ * fra_stream_info.nframes / frame_bytes describe the range.  A count past the stream's end is clipped to it; a
+ * first frame < 0 or past the stream's frame count, or a count < -1, is FRA_E_INVALID. */
 FRA_API int fra_plan_create_ranged(fra_ctx *ctx, const fra_job *job, const int32_t *frame_ranges, fra_plan **out);
 FRA_API int fra_plan_set_raster(fra_plan *plan, const void *raster, int32_t raster_on_device);
 FRA_API int fra_plan_execute(fra_plan *plan);

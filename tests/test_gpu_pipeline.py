@@ -408,14 +408,14 @@ def test_ranged_plan_frames_equal_stream_slices(kind, dtype, level, norm):
 
 def test_ranged_plan_rejects_ranges_outside_the_stream():
     """a (tile, frame range) work item outside its window's stream -- a first frame past the stream's
-    frame count, a count below -1 or past the end -- is rejected at plan creation instead of silently dropping or
-    duplicating frames of the multi-GPU split."""
+    frame count or a count below -1 -- is rejected at plan creation instead of silently dropping or duplicating
+    frames of the multi-GPU split (a count past the end is clipped to it)."""
     ctx = N.default_context(0)
     wins = calculate_tiles(512, 512, 256)  # 16 frames per window
-    ok = [(0, -1), (15, 1), (16, 0), (3, 13)]
+    ok = [(0, -1), (15, 1), (16, 0), (10, 7)]
     plan = N.Plan(ctx, None, False, np.uint16, 1, (512 * 512, 512, 1), wins, 5, 4096, 16, frame_ranges=ok)
     plan.close()
-    for bad in [(17, -1), (0, -5), (10, 7), (-1, 2)]:
+    for bad in [(17, -1), (0, -5), (20, 1), (-1, 2)]:
         with pytest.raises(N.NativeError, match="frame range|first frame"):
             N.Plan(ctx, None, False, np.uint16, 1, (512 * 512, 512, 1), wins, 5, 4096, 16,
                    frame_ranges=[bad] + ok[1:])
