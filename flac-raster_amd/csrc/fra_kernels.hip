@@ -109,8 +109,11 @@ __device__ __forceinline__ double unkey32(uint32_t k) {
   else if constexpr (SRC == ST_I8 || SRC == ST_I16 || SRC == ST_I32) return (double)(int32_t)(k ^ 0x80000000u);
   else return (double)__uint_as_float((k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
 }
-#ifndef FRA_MM_NT  // streaming loads in k_minmax_vec (r05 default: C4 neutral, C3 -0.7 %, C5 quarter -0.6 %; 0 = plain)
-#define FRA_MM_NT 1
+// streaming (nontemporal) row loads in k_minmax_vec: r05's default (C4 neutral, C3 -0.7 %, C5 quarter -0.6 %), off
+// since r06: they fetch 1.105x the raster bytes against 1.007x for plain loads (in-run FETCH_SIZE, C4) and the
+// same-box steps are equal (C4 1.440-1.456 / C3 0.927-0.934 ms either way; profiles/r06_ab_minmax_loads_keep17.txt)
+#ifndef FRA_MM_NT
+#define FRA_MM_NT 0
 #endif
 typedef unsigned int uint4_v __attribute__((ext_vector_type(4)));
 typedef unsigned int uint2_v __attribute__((ext_vector_type(2)));
