@@ -154,6 +154,7 @@ struct AnalyzeSmem {
   int16_t mcoef[kMaxModels][kMaxLpc];
   int8_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
+  double mscore[MAXLAG > 8 ? kMaxModels : 1];  // FRA-1 3.7b window scores (levels 7-8)
   // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
   // partition order (written by porder_search, read by the winner's exact pass)
   uint8_t kbest[kMaxModels][kMaxPart];
@@ -703,6 +704,12 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
           S.mtype[m] = 3; S.morder[m] = o; S.mshift[m] = sh;
 #pragma unroll
           for (int j = 0; j < MAXLAG; j++) S.mcoef[m][j] = ok ? q[j] : 0;
+          if constexpr (MAXLAG > 8) {  // FRA-1 3.7b: the window's score from its chosen order's LD error
+            double eo = errv[0];
+#pragma unroll
+            for (int j = 1; j < MAXLAG; j++) eo = o == j + 1 ? errv[j] : eo;
+            S.mscore[m] = ok ? window_score(eo, ac[0], n, o, prec + sbps) : 0.0;
+          }
         }
         FRA_ROLE_STAMP(15)
       }
@@ -718,6 +725,24 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   else if (fastframe) read_d14(S.smp, t, D);
   else read_x28(S.smp, t, x);
   __syncthreads();  // wave 0's LPC models (mcoef/mshift/mvalid) are visible from here on
+  if constexpr (MAXLAG > 8) {
+    // FRA-1 3.7b (levels 7-8, r06): only cfg.lpc_keep usable LPC models -- the smallest window scores, the lower
+    // window on a tie -- get residual sums and a partition search (oracle analyze_subframe); the others are
+    // invalidated here, before any wave reads the table (published by the barrier below)
+    if (t == 0 && cfg.lpc_keep > 0) {
+      uint32_t keep = 0;
+      for (int r = 0; r < cfg.lpc_keep; r++) {
+        int bm = -1;
+        for (int m = 5; m < nmod; m++)
+          if (S.mvalid[m] && !((keep >> m) & 1u) && (bm < 0 || S.mscore[m] < S.mscore[bm])) bm = m;
+        if (bm < 0) break;
+        keep |= 1u << bm;
+      }
+      for (int m = 5; m < nmod; m++)
+        if (!((keep >> m) & 1u)) S.mvalid[m] = 0;
+    }
+    if constexpr (!B32) __syncthreads();
+  }
   if constexpr (B32) {  // the LPC models' sums held the autocorrelation / LD rows: zero them again
     for (int i = t; i < (kMaxModels - 5) * kMaxPart; i += kThreads) (&S.u.psum[5][0])[i] = 0ull;
     __syncthreads();
@@ -814,8 +839,11 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
     fixed_guess2(S.u.psum, S.mvalid, P, lane, fg1, fg2);
     if (rw == 0 && lane < 5 && lane != fg1 && lane != fg2) S.mvalid[lane] = 0;
   }
-  for (int m = (early ? 5 : 0) + rw; m < nmod; m += 4) {
+  // the models left to search, dealt to the waves in order (r06: compacted, so that 2 LPC models of 6 windows
+  // land on two waves, not both on the wave of their index mod 4)
+  for (int m = early ? 5 : 0, slot = 0; m < nmod; m++) {
     if (!S.mvalid[m] || (m < 5 && m != fg1 && m != fg2)) continue;
+    if ((slot++ & 3) != rw) continue;
     const int o = S.morder[m];
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;

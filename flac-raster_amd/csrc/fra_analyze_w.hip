@@ -288,8 +288,17 @@ __device__ __forceinline__ void wload_lut(const void* base, const WaveDev& wd, i
   for (int kv = 0; kv < NV; kv++) {
     int32_t g[V];
     const bool arith = FRA_W_ARITH == 1 || (FRA_W_ARITH == 2 && (kv & 1));
+    // table byte offsets from the vector's two dwords in 32 bits (r06): indexing by the element of the 8-byte
+    // vector let the compiler form half of the gather addresses with 64-bit adds (v_lshl_add_u64) instead of the
+    // uniform-base + 32-bit-offset form
+    const uint2 xw = __builtin_bit_cast(uint2, x[kv]);
 #pragma unroll
-    for (int e = 0; e < V; e++) g[e] = arith ? wnorm<T>((uint32_t)x[kv].v[e], wn) : lut[(uint32_t)x[kv].v[e]];
+    for (int e = 0; e < V; e++) {
+      constexpr int EB = 8 * (int)sizeof(T);
+      const uint32_t wsrc = e < V / 2 ? xw.x : xw.y;
+      const uint32_t raw = (wsrc >> (EB * (e % (V / 2)))) & ((1u << EB) - 1u);
+      g[e] = arith ? wnorm<T>(raw, wn) : *(const int32_t*)((const char*)lut + (raw << 2));
+    }
     const int i = (lane + 64 * kv) * V;
 #pragma unroll
     for (int h = 0; h < V / 4; h++) {

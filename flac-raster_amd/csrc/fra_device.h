@@ -665,6 +665,16 @@ __device__ inline double order_bits(double e, int n, int o, int overhead) {
   else bps = 0.0;
   return bps * (double)(n - o) + (double)(o * overhead);
 }
+// FRA-1 3.7b window score (== oracle window_score): the expected bits of a window's chosen order o with its LD
+// error taken relative to the window's own energy ac0, so a partial window ranks against the full one
+__device__ inline double window_score(double e, double ac0, int n, int o, int overhead) {
+  const double rel = e / ac0;
+  double bps;
+  if (rel > 0.0) bps = 0.5 * det_log2(0.5 * rel);
+  else if (rel < 0.0) bps = 1e32;
+  else bps = -1e32;
+  return bps * (double)(n - o) + (double)(o * overhead);
+}
 __device__ inline int best_order_by_error(const double* err, int norders, int n, int overhead) {
   double best = 0.0;
   int bo = 1;

@@ -44,18 +44,19 @@ FRA_HD int sidx(const T*, int i) { return smp_stride<T>() + i + (i >> 4) * (smp_
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {
   int32_t max_lpc, max_porder, nsub;
-  int32_t ms;  // mid-side stereo column (levels 1, 2, 4-8)
+  int32_t ms;        // mid-side stereo column (levels 1, 2, 4-8)
+  int32_t lpc_keep;  // FRA-1 3.7b (r06): LPC windows whose residuals are evaluated, by window score (0 = all)
 };
 FRA_HD LevelCfg level_cfg(int level) {
   switch (level < 0 ? 0 : (level > 8 ? 8 : level)) {
-    case 0: return {0, 3, 0, 0};
-    case 1: case 2: return {0, 3, 0, 1};
-    case 3: return {6, 4, 1, 0};
-    case 4: return {8, 4, 1, 1};
-    case 5: return {8, 5, 1, 1};
-    case 6: return {8, 6, 2, 1};
-    case 7: return {12, 6, 2, 1};
-    default: return {12, 6, 3, 1};
+    case 0: return {0, 3, 0, 0, 0};
+    case 1: case 2: return {0, 3, 0, 1, 0};
+    case 3: return {6, 4, 1, 0, 0};
+    case 4: return {8, 4, 1, 1, 0};
+    case 5: return {8, 5, 1, 1, 0};
+    case 6: return {8, 6, 2, 1, 0};
+    case 7: return {12, 6, 2, 1, 2};
+    default: return {12, 6, 3, 1, 2};
   }
 }
 FRA_HD int num_windows(int nsub) {

@@ -174,10 +174,11 @@ typedef struct {
   int max_porder;
   int nsub;     /* 0 = no LPC, 1 = tukey(0.5), 2/3 = subdivide_tukey(2/3) */
   int stereo;   /* mid-side stereo tried for C == 2 (FRA-1 3.1b: streams of <= 16 bps) */
+  int lpc_keep; /* FRA-1 3.7b: LPC windows whose residuals are evaluated (0 = every window) */
 } level_cfg;
 static const level_cfg LEVELS[9] = {
-    {0, 3, 0, 0}, {0, 3, 0, 1}, {0, 3, 0, 1}, {6, 4, 1, 0}, {8, 4, 1, 1},
-    {8, 5, 1, 1}, {8, 6, 2, 1}, {12, 6, 2, 1}, {12, 6, 3, 1}};
+    {0, 3, 0, 0, 0}, {0, 3, 0, 1, 0}, {0, 3, 0, 1, 0}, {6, 4, 1, 0, 0}, {8, 4, 1, 1, 0},
+    {8, 5, 1, 1, 0}, {8, 6, 2, 1, 0}, {12, 6, 2, 1, 2}, {12, 6, 3, 1, 2}};
 
 /* qlp coefficient precision, libFLAC "auto" rule (qlp_coeff_precision == 0):
  * bps <= 16 by blocksize ladder, > 16 -> 13/14/15. */
@@ -357,6 +358,20 @@ static int best_order_by_error(const double *err, int norders, int n, int overhe
     if (o == 1 || bits < best) { best = bits; bo = o; }
   }
   return bo;
+}
+
+/* FRA-1 3.7b override (tests / size studies only): < 0 = the level table's lpc_keep, 0 = every window, k = k */
+static int ora_lpc_keep = -1;
+ORA_API void ora_set_lpc_keep(int k) { ora_lpc_keep = k; }
+/* FRA-1 3.7b window score: the expected bits of the window's chosen order, its LD error taken relative to the
+ * window's own energy (autocorrelation lag 0), so that a partial window -- whose error covers only its segment --
+ * ranks against the full one */
+static double window_score(double e, double ac0, int n, int o, int overhead_per_order) {
+  double rel = e / ac0, bps;
+  if (rel > 0.0) bps = 0.5 * ora_det_log2(0.5 * rel);
+  else if (rel < 0.0) bps = 1e32;
+  else bps = -1e32;
+  return bps * (double)(n - o) + (double)(o * overhead_per_order);
 }
 
 /* ---------------------------------------------------------------- Rice estimation (3.8) */
@@ -559,22 +574,47 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
   int lmax = cfg->max_lpc < n - 1 ? cfg->max_lpc : n - 1;
   if (cfg->nsub > 0 && lmax > 0) {
     int prec = qlp_precision(bps, n);
+    /* 3.7: per window one order chosen by expected bits from the LD errors (libFLAC's non-exhaustive model
+     * search), quantised; a window has a usable model if it has an order and its coefficients quantise */
+    enum { MAXW = 8 };
+    int ordw[MAXW], okw[MAXW], shw[MAXW];
+    int32_t qw[MAXW][32];
+    double scw[MAXW];
     for (int wi = 0; wi < ws->nwin; wi++) {
       const float *win = ws->win + (size_t)wi * n;
       for (int i = 0; i < n; i++) wf[i] = (float)s[i] * win[i];
       double autoc[33];
       ora_autocorr(wf, n, lmax, autoc);
+      okw[wi] = 0;
       if (!(autoc[0] != 0.0)) continue;
       double lp[32 * 32], err[32];
       int nord = ora_levinson(autoc, lmax, lp, err);
-      /* 3.7: one order per window, chosen by expected bits from the LD errors (libFLAC's
-       * non-exhaustive model search) */
-      int olo = 1, ohi = nord;
-      if (nord > 0) { olo = ohi = best_order_by_error(err, nord, n, prec + sbps); }
-      for (int o = olo; o <= ohi; o++) {
-        int32_t q[32];
-        int sh;
-        if (ora_quantize(lp + (o - 1) * 32, o, prec, q, &sh) != 0) continue;
+      if (nord <= 0) continue;
+      int o = best_order_by_error(err, nord, n, prec + sbps);
+      if (ora_quantize(lp + (o - 1) * 32, o, prec, qw[wi], &shw[wi]) != 0) continue;
+      okw[wi] = 1;
+      ordw[wi] = o;
+      scw[wi] = window_score(err[o - 1], autoc[0], n, o, prec + sbps);
+    }
+    /* 3.7b: at levels with lpc_keep > 0 only that many usable models -- the smallest window scores, the lower
+     * window index on a tie -- get residuals and a partition search */
+    const int keepn = ora_lpc_keep >= 0 ? ora_lpc_keep : cfg->lpc_keep;
+    if (keepn > 0) {
+      int keep[MAXW] = {0};
+      for (int r = 0; r < keepn; r++) {
+        int bw = -1;
+        for (int wi = 0; wi < ws->nwin; wi++)
+          if (okw[wi] && !keep[wi] && (bw < 0 || scw[wi] < scw[bw])) bw = wi;
+        if (bw < 0) break;
+        keep[bw] = 1;
+      }
+      for (int wi = 0; wi < ws->nwin; wi++) okw[wi] = okw[wi] && keep[wi];
+    }
+    for (int wi = 0; wi < ws->nwin; wi++) {
+      if (!okw[wi]) continue;
+      {
+        const int o = ordw[wi], sh = shw[wi];
+        const int32_t *q = qw[wi];
         if (!compute_residual(s, n, 3, o, q, sh, r)) continue;
         int po, kk[256];
         uint64_t e = hdr + (uint64_t)o * sbps + 4 + 5 + (uint64_t)o * prec +

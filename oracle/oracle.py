@@ -73,6 +73,7 @@ def lib():
     L.ora_det_log2.restype = C.c_double
     L.ora_sample_rate_for_pixels.argtypes = [C.c_int64]
     L.ora_set_stereo.argtypes = [C.c_int]
+    L.ora_set_lpc_keep.argtypes = [C.c_int]
     _LIB = L
     return L
 
@@ -117,6 +118,11 @@ def crc16(b: bytes) -> int:
 def set_stereo(enable: bool):
     """FRA-1 3.1b mid-side stereo on/off (test hook: report the size gain over independent channels)."""
     lib().ora_set_stereo(1 if enable else 0)
+
+
+def set_lpc_keep(k: int):
+    """FRA-1 3.7b override (test hook): -1 = the level table's rule, 0 = evaluate every LPC window, k = k."""
+    lib().ora_set_lpc_keep(int(k))
 
 
 def encode(samples: np.ndarray, sample_rate: int, level: int = 5, blocksize: int = 4096,

@@ -163,3 +163,33 @@ def test_oracle_mid_side_round_trip_and_gain(golden_dir):
             assert len(ms) <= len(ind)
             assert np.array_equal(O.decode(ms)[0], a.astype(np.int32))
             assert np.array_equal(N.decode(ms)[0], a.astype(np.int32))
+
+
+def test_lpc_window_pruning_costs_little(golden_dir):
+    """FRA-1 3.7b (r06): at levels 7-8 only the two LPC windows with the best window score get residual sums and a
+    partition search (the GPU's k_analyze then sums 2 models instead of up to 6).  On the reference's rasters the
+    rule costs at most 0.1 % of the frame bytes against evaluating every window, the streams decode bit-exactly,
+    and levels <= 6 are unchanged (their level-table entry keeps every window)."""
+    from flac_raster.synth import synth_window
+
+    cases = []
+    for name in ("sample_rgb.tif", "sample_dem.tif", "sample_multispectral.tif"):
+        d, _ = read_geotiff(golden_dir / name)
+        cases.append((O.normalize(d.transpose(1, 2, 0).reshape(-1, d.shape[0]), 16)[0], 16))
+    t = synth_window(5, 20260227, 8, 32768, 32768, 4096, 8192, 256, 512).astype(np.float32)  # C5-like, 32 bps
+    cases.append((O.normalize(t.transpose(1, 2, 0).reshape(-1, 8), 24)[0], 32))
+    try:
+        for a, bps in cases:
+            for level in (6, 7, 8):
+                rule = O.encode(a, 44100, level=level, with_header=False)
+                O.set_lpc_keep(0)
+                every = O.encode(a, 44100, level=level, with_header=False)
+                O.set_lpc_keep(-1)
+                if level == 6:
+                    assert rule == every
+                else:
+                    assert len(rule) <= 1.001 * len(every), (level, bps, len(rule), len(every))
+                dec = O.decode(O.stream_header(a.shape[1], bps, 44100) + rule)[0]
+                assert np.array_equal(dec, a.astype(np.int32))
+    finally:
+        O.set_lpc_keep(-1)
