@@ -41,6 +41,11 @@ FRA_HD constexpr int smp_words() { return (kMaxBlock / kChunk + 1) * smp_stride<
 template <typename T>
 FRA_HD int sidx(const T*, int i) { return smp_stride<T>() + i + (i >> 4) * (smp_stride<T>() - kChunk); }
 
+// FRA-1 3.7b windows kept at levels 7-8 (the oracle's level table must agree).  r06: 2 then 1 -- C5 analysis 88.2 ->
+// 72.7 -> 67.7 ms, frame bytes +0.015 % -> +0.026 % against evaluating all 6 windows (profiles/r06_ab_c5_window_pruning.txt)
+#ifndef FRA_LPC_KEEP78
+#define FRA_LPC_KEEP78 1
+#endif
 // libFLAC 1.4.3 compression-level table (docs/sonos-pyflac.txt:6926-6934)
 struct LevelCfg {
   int32_t max_lpc, max_porder, nsub;
@@ -55,8 +60,8 @@ FRA_HD LevelCfg level_cfg(int level) {
     case 4: return {8, 4, 1, 1, 0};
     case 5: return {8, 5, 1, 1, 0};
     case 6: return {8, 6, 2, 1, 0};
-    case 7: return {12, 6, 2, 1, 2};
-    default: return {12, 6, 3, 1, 2};
+    case 7: return {12, 6, 2, 1, FRA_LPC_KEEP78};
+    default: return {12, 6, 3, 1, FRA_LPC_KEEP78};
   }
 }
 FRA_HD int num_windows(int nsub) {

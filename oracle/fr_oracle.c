@@ -178,7 +178,7 @@ typedef struct {
 } level_cfg;
 static const level_cfg LEVELS[9] = {
     {0, 3, 0, 0, 0}, {0, 3, 0, 1, 0}, {0, 3, 0, 1, 0}, {6, 4, 1, 0, 0}, {8, 4, 1, 1, 0},
-    {8, 5, 1, 1, 0}, {8, 6, 2, 1, 0}, {12, 6, 2, 1, 2}, {12, 6, 3, 1, 2}};
+    {8, 5, 1, 1, 0}, {8, 6, 2, 1, 0}, {12, 6, 2, 1, 1}, {12, 6, 3, 1, 1}};
 
 /* qlp coefficient precision, libFLAC "auto" rule (qlp_coeff_precision == 0):
  * bps <= 16 by blocksize ladder, > 16 -> 13/14/15. */

@@ -166,8 +166,8 @@ def test_oracle_mid_side_round_trip_and_gain(golden_dir):
 
 
 def test_lpc_window_pruning_costs_little(golden_dir):
-    """FRA-1 3.7b (r06): at levels 7-8 only the two LPC windows with the best window score get residual sums and a
-    partition search (the GPU's k_analyze then sums 2 models instead of up to 6).  On the reference's rasters the
+    """FRA-1 3.7b (r06): at levels 7-8 only the LPC window with the best window score gets residual sums and a
+    partition search (the GPU's k_analyze then sums 1 model instead of up to 6).  On the reference's rasters the
     rule costs at most 0.1 % of the frame bytes against evaluating every window, the streams decode bit-exactly,
     and levels <= 6 are unchanged (their level-table entry keeps every window)."""
     from flac_raster.synth import synth_window
