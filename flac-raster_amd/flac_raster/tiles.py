@@ -55,22 +55,65 @@ def frames_of(tile: Tuple[int, int, int, int], blocksize: int = 4096) -> int:
     return -(-(tile[2] * tile[3]) // blocksize)
 
 
+# What holding partial last frames (n < blocksize) costs a rank, in full frames: those subframes run as ONE separate,
+# latency-bound k_analyze launch per execute beside the per-wave analysis of the full frames, whatever their number.
+# Measured on the C4 8-way split (r06, profiles/r06_shards_partial_cost.txt): the one rank holding the scene's only
+# partial frame (the 740^2 corner tile) stepped ~0.012 ms (~6 %, about 240 frames of analysis) slower than the others.
+PARTIAL_FRAME_COST = 256
+
+
 def frame_split(tiles: Sequence[Tuple[int, int, int, int]], parts: int,
-                blocksize: int = 4096, stride: int = 1) -> List[List[Tuple[int, int, int]]]:
-    """Work items of equal size for ``parts`` ranks ((tile, frame range) items): the frames
-    of all tiles in tile order, cut into ``parts`` contiguous runs of equal frame count; part k gets a list
-    of (tile index, first frame, frame count) -- whole tiles, plus at most a partial tile at each end.  The
-    frames of one tile, concatenated over the parts in order, are that tile's stream.
+                blocksize: int = 4096, stride: int = 1,
+                partial_cost: int = PARTIAL_FRAME_COST) -> List[List[Tuple[int, int, int]]]:
+    """Work items of equal cost for ``parts`` ranks ((tile, frame range) items): the frames of all
+    tiles in tile order, cut into ``parts`` contiguous runs; part k gets a list of (tile index, first frame, frame
+    count) -- whole tiles, plus at most a partial tile at each end.  The frames of one tile, concatenated over the
+    parts in order, are that tile's stream.  A part's cost is its frame count, plus ``partial_cost`` if it holds a
+    tile's partial last frame (0: equal frame counts); the cuts are refined over a few passes (the parts holding
+    partial frames depend on the cuts) and the pass with the smallest largest cost is kept.
 
     ``stride`` > 1 visits the tiles as i = 0, s, 2s, ..., then 1, 1 + s, ... (tile index mod s first), so each
     part's run samples the whole scene instead of one band of it: content that varies across the scene (a
-    no-data corner, water, cloud) spreads over the parts, while the frame counts stay equal."""
+    no-data corner, water, cloud) spreads over the parts, while the costs stay equal."""
     counts = [frames_of(t, blocksize) for t in tiles]
+    order = sorted(range(len(tiles)), key=lambda j: (j % max(1, stride), j))
     total = sum(counts)
+    # the global frame index of every partial last frame, in visiting order
+    partial_at, pos = [], 0
+    for i in order:
+        pos += counts[i]
+        if (tiles[i][2] * tiles[i][3]) % blocksize:
+            partial_at.append(pos - 1)
+    # (bounded by a quarter part's frames: no part can be left empty)
+    pc = max(0, min(partial_cost, total // (4 * max(1, parts))))
+
+    def cut(holds):  # cuts giving part k a frame count of (total + pc |P|) / parts - pc [k in P]
+        t = total + pc * sum(holds)
+        c, acc = [0], 0
+        for k in range(parts):
+            acc += (t * (k + 1) // parts - t * k // parts) - pc * holds[k]
+            c.append(min(total, max(c[-1], acc)))
+        c[-1] = total
+        return c
+
+    def holders(c):
+        return [int(any(c[k] <= f < c[k + 1] for f in partial_at)) for k in range(parts)]
+
+    def worst(c):  # the largest part cost of cuts c
+        h = holders(c)
+        return max(c[k + 1] - c[k] + pc * h[k] for k in range(parts))
+
     cuts = [total * k // parts for k in range(parts + 1)]
+    if pc and partial_at:
+        cands = [cuts]
+        for _ in range(4):  # a cut next to a partial frame can flip its holder: keep the best of the passes
+            cands.append(cut(holders(cands[-1])))
+            if cands[-1] == cands[-2]:
+                break
+        cuts = min(cands, key=worst)
     out: List[List[Tuple[int, int, int]]] = [[] for _ in range(parts)]
     base = 0
-    for i in sorted(range(len(tiles)), key=lambda j: (j % max(1, stride), j)):
+    for i in order:
         n = counts[i]
         for k in range(parts):
             a, b = max(base, cuts[k]), min(base + n, cuts[k + 1])

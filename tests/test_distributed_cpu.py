@@ -81,7 +81,7 @@ def test_distributed_container_identical(tmp_path, world, tile, split):
 
 @pytest.mark.parametrize("strided", [False, True])
 def test_frame_split_partitions_frames(strided):
-    from flac_raster.tiles import calculate_tiles, frame_split, frames_of
+    from flac_raster.tiles import PARTIAL_FRAME_COST, calculate_tiles, frame_split, frames_of
 
     tiles = calculate_tiles(10980, 10980, 1024)
     F = sum(frames_of(t) for t in tiles)
@@ -89,7 +89,17 @@ def test_frame_split_partitions_frames(strided):
         parts = frame_split(tiles, world, stride=world if strided else 1)
         if strided and world == 8:  # every part's run spans the scene (tiles of every row band)
             assert all(max(i for i, _, _ in p) - min(i for i, _, _ in p) > len(tiles) // 2 for p in parts)
-        assert max(sum(n for _, _, n in p) for p in parts) - min(sum(n for _, _, n in p) for p in parts) <= 1
+        # equal cost: the frames, + PARTIAL_FRAME_COST for the part holding the corner tile's partial last frame
+        def cost(p):
+            return sum(n for _, _, n in p) + (PARTIAL_FRAME_COST if any(
+                f0 + n == frames_of(tiles[i]) and (tiles[i][2] * tiles[i][3]) % 4096 for i, f0, n in p) else 0)
+        eq = frame_split(tiles, world, stride=world if strided else 1, partial_cost=0)
+        assert max(map(cost, parts)) <= max(map(cost, eq))  # never worse than equal frame counts
+        if world > 1 and not strided:  # the part holding the partial frame gets fewer frames
+            owner = next(k for k, p in enumerate(parts) if any(i == len(tiles) - 1 for i, _, _ in p))
+            assert sum(n for _, _, n in parts[owner]) < min(sum(n for _, _, n in p) for k, p in enumerate(parts)
+                                                            if k != owner)
+        assert max(sum(n for _, _, n in p) for p in eq) - min(sum(n for _, _, n in p) for p in eq) <= 1
         seen = {}
         for p in parts:
             for i, f0, n in p:
