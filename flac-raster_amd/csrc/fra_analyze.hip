@@ -154,6 +154,7 @@ struct AnalyzeSmem {
   int16_t mcoef[kMaxModels][kMaxLpc];
   int8_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
+  unsigned long long mtot[kMaxModels];  // block total of 2|r| of each searched model (FRA-1 3.7c)
   double mscore[MAXLAG > 8 ? kMaxModels : 1];  // FRA-1 3.7b window scores (levels 7-8)
   // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
   // partition order (written by porder_search, read by the winner's exact pass)
@@ -338,15 +339,33 @@ __device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kM
   g2 = __builtin_amdgcn_readfirstlane(h2);
 }
 
+// FRA-1 3.7c (r06): a FIXED candidate whose block total of 2|r| is not below the smallest block total of the LPC
+// models evaluated drops out of the winner choice (oracle analyze_subframe).  The totals are the root nodes of the
+// models' partition searches (S.mtot; the FIXED searches may have run speculatively, during Levinson-Durbin).
+// Wave-uniform: the mask of the FIXED models to drop.
+__device__ __forceinline__ uint32_t fixed_gate(const unsigned long long* mtot, const int8_t* mvalid, int nmod) {
+  unsigned long long lt = ~0ull;
+  for (int m = 5; m < nmod; m++)
+    if (__builtin_amdgcn_readfirstlane(mvalid[m]) && mtot[m] < lt) lt = mtot[m];
+  uint32_t drop = 0;
+  if (lt != ~0ull)
+    for (int m = 0; m < 5; m++)
+      if (__builtin_amdgcn_readfirstlane(mvalid[m]) && mtot[m] >= lt) drop |= 1u << m;
+  return drop;
+}
+
 // Every partition order of one model's finest sums psum[0, 2^P) in one wave (porder_search_reg,
 // fra_device.h: node sums by the upper-lane DPP tree and ds_bpermute, no LDS); kout[j], j < 2^bp, receives
 // partition j's Rice parameter at the chosen order
 __device__ __forceinline__ void porder_search(const unsigned long long* psum, int P, int pm, int n, int o, int lane,
-                                              uint64_t& best_out, int& bp_out, uint8_t* kout = nullptr) {
+                                              uint64_t& best_out, int& bp_out, uint8_t* kout = nullptr,
+                                              unsigned long long* tot = nullptr) {
   const uint64_t Sv = lane < (1 << P) ? psum[lane] : 0ull;
   uint32_t kreg = 0;
-  porder_search_reg(Sv, P, pm, n, o, lane, best_out, bp_out, kreg);
+  uint64_t total = 0;
+  porder_search_reg(Sv, P, pm, n, o, lane, best_out, bp_out, kreg, &total);
   if (kout && (bp_out == 6 || lane < (1 << bp_out))) kout[lane] = (uint8_t)kreg;
+  if (tot && lane == 0) *tot = total;  // the model's block total of 2|r| (FRA-1 3.7c)
 }
 
 // VERBATIM subframe written word by word straight to its slot (32-bps path, whose LDS bit buffer aliases
@@ -649,7 +668,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
           const int pm = max_porder(n, m, cfg.max_porder);
           uint64_t best = 0;
           int bp = pm;
-          porder_search(S.u.psum[m], P, pm, n, m, lane, best, bp, S.kbest[m]);
+          porder_search(S.u.psum[m], P, pm, n, m, lane, best, bp, S.kbest[m], &S.mtot[m]);
           if (lane == 0) {
             S.mest[m] = (uint32_t)(hdr + (uint64_t)m * sbps + best);
             S.mporder[m] = bp;
@@ -848,7 +867,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
     const int pm = max_porder(n, o, cfg.max_porder);
     uint64_t best = 0;
     int bp = pm;
-    porder_search(S.u.psum[m], P, pm, n, o, lane, best, bp, S.kbest[m]);
+    porder_search(S.u.psum[m], P, pm, n, o, lane, best, bp, S.kbest[m], &S.mtot[m]);
     if (lane == 0) {
       S.mest[m] = (uint32_t)(hdr + (uint64_t)o * sbps + (S.mtype[m] == 3 ? 9 + (uint64_t)o * prec : 0) + best);
       S.mporder[m] = bp;
@@ -868,8 +887,9 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
       // ---- 6+7, fast frames: every wave derives the winner and the partition Rice parameters
       // itself (same integers in every wave: no wave-0 section + broadcast barrier), exact sums by LDS
       // atomics, the same refinement in every wave, then the encoder.  4 barriers instead of 7.
+      const uint32_t drop = fixed_gate(S.mtot, S.mvalid, nmod);  // FRA-1 3.7c
       uint32_t key = ~0u;
-      if (lane < nmod && S.mvalid[lane]) key = (S.mest[lane] << 5) | (uint32_t)lane;
+      if (lane < nmod && S.mvalid[lane] && !((drop >> lane) & 1u)) key = (S.mest[lane] << 5) | (uint32_t)lane;
       const int m = (int)(wave_min32(key) & 31u);
       const int type = __builtin_amdgcn_readfirstlane(S.mtype[m]);
       const int o = __builtin_amdgcn_readfirstlane(S.morder[m]);
@@ -1098,8 +1118,9 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
     }
   }
   if (rw == 0) {  // winner = first minimal estimate: argmin over (estimate, model index)
+    const uint32_t drop = fixed_gate(S.mtot, S.mvalid, nmod);  // FRA-1 3.7c
     uint32_t key = ~0u;
-    if (lane < nmod && S.mvalid[lane]) key = (S.mest[lane] << 5) | (uint32_t)lane;
+    if (lane < nmod && S.mvalid[lane] && !((drop >> lane) & 1u)) key = (S.mest[lane] << 5) | (uint32_t)lane;
     key = wave_min32(key);
     if (lane == 0) S.winner = (int)(key & 31u);
   }

@@ -190,7 +190,8 @@ __device__ inline int levinson_keep(const double (&ac)[MAXLAG + 1], int max_orde
 
 // FRA-1 3.7 FIXED candidates from register partition sums (lane p < 2^P: partition p of order k) ==
 // fixed_guess2 (fra_analyze.hip) with every order valid (n = 4096)
-__device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, int lane, int& g1, int& g2) {
+__device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, int lane, int& g1, int& g2,
+                                               uint64_t& t1, uint64_t& t2) {
   uint64_t T[5];
   bool small = true;
   uint32_t pv[5];
@@ -225,6 +226,8 @@ __device__ __forceinline__ void fixed_guess2_w(const uint32_t (&ps)[5], int P, i
   }
   g1 = __builtin_amdgcn_readfirstlane(h1);
   g2 = __builtin_amdgcn_readfirstlane(h2);
+  t1 = b1;  // their block totals (FRA-1 3.7c)
+  t2 = b2;
 }
 
 // LUT fast load of one channel of a full frame into the swizzled chunks (load_lut_full_t, per wave):
@@ -541,7 +544,8 @@ k_analyze_w(JobArgs a, int src) {
   // ---- 5a. FIXED candidates (3.7): the two orders with the smallest totals; their partition sums stay
   // in registers for the candidate loop below
   int g1, g2;
-  fixed_guess2_w(pfix, P, lane, g1, g2);
+  uint64_t gt1, gt2;
+  fixed_guess2_w(pfix, P, lane, g1, g2, gt1, gt2);
   uint32_t pf1 = 0, pf2 = 0;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
@@ -727,10 +731,12 @@ k_analyze_w(JobArgs a, int src) {
   }
 #endif
 
-  // ---- 4+5. the candidates in model order -- FIXED g1, g2, then each window's LPC model -- one partition
-  // search each (one code body); an LPC model first gets its residual sums at the finest partitions.
-  // The last window with a model is summed last: its pass replaces each chunk's samples in LDS by the
-  // chunk's zig-zag residuals (int16 pairs), which the exact pass and the encoder then read instead of
+  // ---- 4+5. the candidates -- each window's LPC model, then FIXED g1, g2 (r06: LPC first, so that FRA-1 3.7c can drop
+  // a FIXED candidate whose block total is not below the LPC models' smallest one before its search; the winner is
+  // still the first minimal estimate in model order, FIXED first: offer() compares (estimate, model index)) -- one
+  // partition search each (one code body); an LPC model first gets its residual sums at the finest partitions.
+  // The keep window's model is summed last among the LPC models: its pass replaces each chunk's samples in LDS by
+  // the chunk's zig-zag residuals (int16 pairs), which the exact pass and the encoder then read instead of
   // recomputing the predictor twice (fallback: the samples are loaded again)
   // windows with a usable model (lanes 24 + wi of mv with an order)
   const uint32_t okm = (uint32_t)(__ballot(lane >= 24 && lane < 24 + kWinW && (mv >> 8) != 0) >> 24);
@@ -744,16 +750,18 @@ k_analyze_w(JobArgs a, int src) {
   uint64_t hk = 0;  // bit 16 of the kept residuals: bit 16 j + jj = chunk 64 j + lane's residual jj
   bool hk_any = false;  // (wave-uniform) some kept residual has bit 16
   uint32_t w4[4] = {0, 0, 0, 0};  // samples 0..7 (the warm-up), saved before chunk 0 is overwritten
+  uint64_t lpcT = ~0ull;  // the smallest block total of 2|r| of the LPC models summed (FRA-1 3.7c)
 #pragma unroll 1
-  for (int ci = 0; ci < 2 + nlpc; ci++) {
+  for (int ci = 0; ci < nlpc + 2; ci++) {
     int m, o, sh = 0, type = 2;
     int32_t qm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t psum = 0;
-    if (ci < 2) {
-      m = o = ci == 0 ? g1 : g2;
-      psum = ci == 0 ? pf1 : pf2;
+    if (ci >= nlpc) {  // FIXED g1, g2 -- dropped when not below the LPC models' block total (3.7c)
+      m = o = ci == nlpc ? g1 : g2;
+      if (o < 0 || (lpcT != ~0ull && (ci == nlpc ? gt1 : gt2) >= lpcT)) continue;
+      psum = ci == nlpc ? pf1 : pf2;
     } else {
-      const int wi = (ci - 2 + keep_wi + 1) % nlpc;  // the keep window last (nlpc >= 1 here)
+      const int wi = (ci + keep_wi + 1) % nlpc;  // the keep window last (nlpc >= 1 here)
       if (!((okm >> wi) & 1u)) continue;  // no order / not quantisable
       const uint32_t inf = (uint32_t)__builtin_amdgcn_readlane((int)mv, 24 + wi);
       o = (int)(inf >> 8);
@@ -825,6 +833,13 @@ k_analyze_w(JobArgs a, int src) {
           psum = pj == j ? gs : psum;
         }
       }
+      // the model's block total (lanes >= 2^P hold 0)
+      uint64_t tv = psum;
+      tv = up_add64<0>(tv); tv = up_add64<1>(tv); tv = up_add64<2>(tv);
+      tv = up_add64<3>(tv); tv = up_add64<4>(tv); tv = up_add64<5>(tv);
+      const uint64_t T = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tv >> 32), 63) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tv, 63);
+      lpcT = T < lpcT ? T : lpcT;
     }
     constexpr int pm = P;  // max_porder(n, o, cfg.max_porder) == P for n = 4096, o <= 8
     uint64_t best;

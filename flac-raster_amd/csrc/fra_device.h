@@ -1021,7 +1021,7 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src) {
 // Same nodes, tree, tie rule and outputs as the oracle's per-level loop (p = pm..0, keep '<='); every node sum
 // < 2^29 runs in 32-bit arithmetic (rice_pick32, bit-identical); kreg lane j < 2^bp = partition j's Rice parameter
 __device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, int n, int o, int lane, uint64_t& best_out,
-                                                int& bp_out, uint32_t& kreg) {
+                                                int& bp_out, uint32_t& kreg, uint64_t* total_out = nullptr) {
   const int p = lane ? 31 - __clz(lane) : 0;  // this lane's level; j = lane - 2^p
   const int jn = lane - (1 << p);
   uint32_t bits32 = 0;
@@ -1045,6 +1045,7 @@ __device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, in
     FRA_NODE_STEP32(0) FRA_NODE_STEP32(1) FRA_NODE_STEP32(2)
     FRA_NODE_STEP32(3) FRA_NODE_STEP32(4) FRA_NODE_STEP32(5)
 #undef FRA_NODE_STEP32
+    if (total_out) *total_out = (uint32_t)__builtin_amdgcn_readlane((int)nv, 1);  // node (0, 0): the block total
     {  // every lane (no exec masking), the result kept where the lane holds a node of a searched level
       int kq;
       uint32_t bq;
@@ -1073,6 +1074,9 @@ __device__ __forceinline__ void porder_search_reg(uint64_t Sv, int P, int pm, in
     FRA_NODE_STEP(0) FRA_NODE_STEP(1) FRA_NODE_STEP(2)
     FRA_NODE_STEP(3) FRA_NODE_STEP(4) FRA_NODE_STEP(5)
 #undef FRA_NODE_STEP
+    if (total_out)
+      *total_out = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(nv >> 32), 1) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nv, 1);
     if (lane >= 1 && p <= P && p <= pm) {
       uint64_t bits;
       rice_pick((uint64_t)((n >> p) - (jn == 0 ? o : 0)), nv, kn, bits);

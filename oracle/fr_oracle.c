@@ -362,6 +362,9 @@ static int best_order_by_error(const double *err, int norders, int n, int overhe
 
 /* FRA-1 3.7b override (tests / size studies only): < 0 = the level table's lpc_keep, 0 = every window, k = k */
 static int ora_lpc_keep = -1;
+/* FRA-1 3.7c override (tests / size studies only): 1 = every FIXED candidate is searched (pre-r06 rule) */
+static int ora_fixed_all = 0;
+ORA_API void ora_set_fixed_all(int on) { ora_fixed_all = on != 0; }
 ORA_API void ora_set_lpc_keep(int k) { ora_lpc_keep = k; }
 /* FRA-1 3.7b window score: the expected bits of the window's chosen order, its LD error taken relative to the
  * window's own energy (autocorrelation lag 0), so that a partial window -- whose error covers only its segment --
@@ -545,32 +548,26 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
   int bk[256];
   uint64_t best_est = 0;
 
-  /* candidate list: the two FIXED orders 0..4 with the smallest sum of 2|r| over the block (first
-   * minimum first, like libFLAC's fixed-order guess but keeping the runner-up), then one LPC order
-   * per window */
+  /* candidates (3.7): the two FIXED orders 0..4 with the smallest block total of 2|r| (first minimum first, like
+   * libFLAC's fixed-order guess but keeping the runner-up), then one LPC order per window.  Winner (3.8): the first
+   * minimal estimate in that order (FIXED g1, g2 by order, then the windows); a FIXED candidate whose block total
+   * is not below the smallest block total of the LPC models evaluated is dropped (3.7c).  The LPC models are
+   * evaluated first so their totals are known, the order of the comparison is kept by the tie rule below. */
   int fmax = n - 1 < 4 ? n - 1 : 4;
   int fg1 = -1, fg2 = -1;
+  uint64_t fT[5] = {0, 0, 0, 0, 0};
   {
     uint64_t bt1 = 0, bt2 = 0;
     for (int o = 0; o <= fmax; o++) {
       if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue;
       uint64_t T = 0;
       for (int i = o; i < n; i++) T += 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
+      fT[o] = T;
       if (fg1 < 0 || T < bt1) { bt2 = bt1; fg2 = fg1; bt1 = T; fg1 = o; }
       else if (fg2 < 0 || T < bt2) { bt2 = T; fg2 = o; }
     }
   }
-  for (int o = 0; o <= fmax; o++) {
-    if (o != fg1 && o != fg2) continue;
-    if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue; /* 32-bps: residual outside int32 */
-    int po, kk[256];
-    uint64_t e = hdr + (uint64_t)o * sbps + residual_estimate(r, n, o, cfg->max_porder, &po, kk);
-    if (btype < 0 || e < best_est) {
-      best_est = e; btype = 2; border = o; bporder = po;
-      memcpy(bk, kk, sizeof(int) * (1 << po));
-      memcpy(rbest, r, sizeof(int64_t) * n);
-    }
-  }
+  uint64_t lpcT = UINT64_MAX; /* smallest block total of 2|r| over the LPC models evaluated (3.7c) */
   int lmax = cfg->max_lpc < n - 1 ? cfg->max_lpc : n - 1;
   if (cfg->nsub > 0 && lmax > 0) {
     int prec = qlp_precision(bps, n);
@@ -612,20 +609,34 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
     }
     for (int wi = 0; wi < ws->nwin; wi++) {
       if (!okw[wi]) continue;
-      {
-        const int o = ordw[wi], sh = shw[wi];
-        const int32_t *q = qw[wi];
-        if (!compute_residual(s, n, 3, o, q, sh, r)) continue;
-        int po, kk[256];
-        uint64_t e = hdr + (uint64_t)o * sbps + 4 + 5 + (uint64_t)o * prec +
-                     residual_estimate(r, n, o, cfg->max_porder, &po, kk);
-        if (e < best_est) {
-          best_est = e; btype = 3; border = o; bporder = po; bshift = sh; bprec = prec;
-          memcpy(bcoef, q, sizeof(int32_t) * o);
-          memcpy(bk, kk, sizeof(int) * (1 << po));
-          memcpy(rbest, r, sizeof(int64_t) * n);
-        }
+      const int o = ordw[wi], sh = shw[wi];
+      const int32_t *q = qw[wi];
+      if (!compute_residual(s, n, 3, o, q, sh, r)) continue;
+      uint64_t T = 0;
+      for (int i = o; i < n; i++) T += 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
+      if (T < lpcT) lpcT = T;
+      int po, kk[256];
+      uint64_t e = hdr + (uint64_t)o * sbps + 4 + 5 + (uint64_t)o * prec +
+                   residual_estimate(r, n, o, cfg->max_porder, &po, kk);
+      if (btype < 0 || e < best_est) {
+        best_est = e; btype = 3; border = o; bporder = po; bshift = sh; bprec = prec;
+        memcpy(bcoef, q, sizeof(int32_t) * o);
+        memcpy(bk, kk, sizeof(int) * (1 << po));
+        memcpy(rbest, r, sizeof(int64_t) * n);
       }
+    }
+  }
+  for (int o = 0; o <= fmax; o++) {
+    if (o != fg1 && o != fg2) continue;
+    if (!ora_fixed_all && lpcT != UINT64_MAX && fT[o] >= lpcT) continue; /* 3.7c */
+    if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue; /* 32-bps: residual outside int32 */
+    int po, kk[256];
+    uint64_t e = hdr + (uint64_t)o * sbps + residual_estimate(r, n, o, cfg->max_porder, &po, kk);
+    /* FIXED precedes every LPC model in candidate order (wins a tie with one), and g1/g2 go by order */
+    if (btype < 0 || e < best_est || (btype == 3 && e == best_est)) {
+      best_est = e; btype = 2; border = o; bporder = po;
+      memcpy(bk, kk, sizeof(int) * (1 << po));
+      memcpy(rbest, r, sizeof(int64_t) * n);
     }
   }
   /* 3.9 exact bits for the winner, compare with verbatim */
