@@ -63,6 +63,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-leve
 SIMDS = 256 * 4          # 256 CUs x 4 SIMD-32
 VALU_CYC = 2             # SIMD cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
 XCDS = 8                 # GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs
+SETTLE = 16              # untimed executes of plan set-up, before the --warmup steps (reported as settle_executes)
 
 
 def tiles(H, W, t):
@@ -578,6 +579,11 @@ def main():
     plan.sync()
     first_ms = (time.perf_counter() - t0) * 1e3
     first_inst = (17 if plan.flags() & 8 else 16) if wave_plan else None
+    # plan set-up, before the W warmup steps: SETTLE executes bring the device to its steady state (r06,
+    # profiles/r06_keep17_order.txt: after 4 executes the next 20 still ran ~3-4 % slower than later segments of 20)
+    for _ in range(SETTLE):
+        plan.execute()
+    plan.sync()
     for _ in range(args.warmup):
         plan.execute()
     plan.sync()
@@ -761,6 +767,7 @@ def main():
             **({"rehearsal": rehearsal} if rehearsal else {}),
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_executes": 1 + SETTLE,
             "ms_per_step": round(T / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
