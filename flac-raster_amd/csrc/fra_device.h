@@ -291,6 +291,7 @@ __device__ __forceinline__ void load_channel_t(const void* base, const WaveDev& 
       vmax = max(vmax, v);
     }
   }
+  FRA_LOAD_STAMP(13, (int)orv)  // (diagnostic build only: normalised values stored)
 }
 // Fast path of the 16-bit instance (full 4096-sample frames of a <= 16-bit integer raster, 8-byte vectors,
 // host-checked 32-bit byte offsets JobArgs::off32): per lane 32-bit offsets from a uniform frame-row base
