@@ -140,6 +140,17 @@ def test_edge_cases():
     check_windows(f, [(0, 0, 64, 80)], 8, 24)
     allnan = np.full((1, 40, 40), np.nan, np.float32)
     check_windows(allnan, [(0, 0, 40, 40)], 5, 16)
+    # r06 (float32 quotient by Markstein's correction, IEEE division only for an infinite range): -inf in one tile,
+    # a one-ulp range, subnormal and huge values, against the oracle's IEEE division
+    g = synth_window(5, 10, 2, 64, 96)
+    g[0, 3, 70] = -np.inf
+    g[1, 40:, :48] = np.float32(1e-40)  # subnormal float32
+    g[1, 40:, 48:] = np.float32(3e38)
+    check_windows(g, [(0, 0, 64, 48), (0, 48, 64, 48), (32, 0, 32, 96)], 5, 24)
+    ulp = np.full((1, 32, 64), np.float32(0.15), np.float32)
+    ulp[0, ::3, ::5] = np.nextafter(np.float32(0.15), np.float32(1))
+    check_windows(ulp, [(0, 0, 32, 64)], 8, 24)
+    check_windows(ulp, [(0, 0, 32, 64)], 5, 16)
 
 
 def test_small_blocksizes():
