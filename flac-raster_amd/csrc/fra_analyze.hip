@@ -155,6 +155,7 @@ struct AnalyzeSmem {
   int8_t mtype[kMaxModels], morder[kMaxModels], mshift[kMaxModels], mvalid[kMaxModels], mporder[kMaxModels];
   uint32_t mest[kMaxModels];
   unsigned long long mtot[kMaxModels];  // block total of 2|r| of each searched model (FRA-1 3.7c)
+  unsigned long long ftot_s[5];  // FIXED orders' totals over the even 1024-sample quarters (FRA-1 3.7d)
   double mscore[MAXLAG > 8 ? kMaxModels : 1];  // FRA-1 3.7b window scores (levels 7-8)
   // 16-bit fast path: Rice parameter estimate of every partition at each searched model's best
   // partition order (written by porder_search, read by the winner's exact pass)
@@ -292,35 +293,25 @@ __device__ __forceinline__ uint32_t lpc_abs16(const int32_t* x, const int32_t* q
   return acc;
 }
 
-// FRA-1 3.7: the two FIXED orders with the smallest block total of 2|r| (first minimum first; invalid
-// orders skipped) == oracle fg1/fg2.  Wave-uniform, every wave may run it.
-__device__ __forceinline__ void fixed_guess2(const unsigned long long (*psum)[kMaxPart], const int8_t* mvalid, int P,
-                                             int lane, int& g1, int& g2) {
-  uint64_t T[5], pv[5];
-  bool small = true;
+// wave-uniform sum of a 64-bit value over the wave (upper-lane DPP tree, lane 63's result broadcast)
+__device__ __forceinline__ uint64_t wave_sum_u64_dpp(uint64_t v) {
+  v = up_add64<0>(v); v = up_add64<1>(v); v = up_add64<2>(v);
+  v = up_add64<3>(v); v = up_add64<4>(v); v = up_add64<5>(v);
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+// FRA-1 3.7 / 3.7d: the two FIXED orders with the smallest total of 2|r| over the even 1024-sample quarters of the
+// block (ftot_s; first minimum first; invalid orders skipped) == oracle fg1/fg2.  Wave-uniform, every wave may run it.
+__device__ __forceinline__ void fixed_guess2(const unsigned long long* ftot_s, const int8_t* mvalid, int lane,
+                                             int& g1, int& g2) {
+  uint64_t T[5];
 #pragma unroll
   for (int k = 0; k < 5; k++) {
-    pv[k] = lane < (1 << P) ? psum[k][lane] : 0ull;
-    small = small && pv[k] < (1ull << 25);
+    const uint64_t v = ftot_s[k];
+    T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
   }
-  if (__all(small)) {  // <= 64 partitions of < 2^25 each: the block totals fit 32 bits (1-instruction DPP adds)
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      uint32_t v = (uint32_t)pv[k];
-      v = up_add32<0>(v); v = up_add32<1>(v); v = up_add32<2>(v);
-      v = up_add32<3>(v); v = up_add32<4>(v); v = up_add32<5>(v);
-      T[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      uint64_t v = pv[k];
-      v = up_add64<0>(v); v = up_add64<1>(v); v = up_add64<2>(v);
-      v = up_add64<3>(v); v = up_add64<4>(v); v = up_add64<5>(v);
-      T[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
-    }
-  }
+  (void)lane;
   // branch-free selects on uniform values (a branchy form let the compiler merge g1/g2 into a
   // dynamically indexed private array, i.e. scratch memory)
   int h1 = -1, h2 = -1;
@@ -474,6 +465,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   }
   // residual partition sums are accumulated from phase 3 on (FIXED sums overlap wave 0's LPC work)
   for (int i = t; i < kMaxModels * kMaxPart; i += kThreads) (&S.u.psum[0][0])[i] = 0ull;
+  if (t < 5) S.ftot_s[t] = 0ull;
   orv = wave_or32(orv);
   const uint32_t kmin = wave_min32((uint32_t)vmin ^ 0x80000000u);   // order-preserving keys
   const uint32_t kmax = ~wave_min32(~((uint32_t)vmax ^ 0x80000000u));
@@ -572,6 +564,12 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
         s32 = sad_acc(ab, bb, s32);
       }
       if (i0 < n && s32) atomicAdd(&S.u.psum[k][pidx0], 2ull * s32);
+      // (3.7d) the even quarters' total: a whole wave's 16-sample chunks lie in one quarter (t >> 6 = the wave): one
+      // wave sum and one LDS atomic per even wave (64 same-address lanes would serialise)
+      if (!(wv & 1)) {
+        const uint64_t ws = wave_sum_u64_dpp(i0 < n ? 2ull * s32 : 0ull);
+        if (lane == 0 && ws) atomicAdd(&S.ftot_s[k], (unsigned long long)ws);
+      }
     }
   }
   FRA_STOP(9)
@@ -661,7 +659,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
       }
       if (early && (rw == nldw || rw == nldw + 1)) {
         int g1, g2;
-        fixed_guess2(S.u.psum, S.mvalid, P, lane, g1, g2);
+        fixed_guess2(S.ftot_s, S.mvalid, lane, g1, g2);
         if (rw == nldw && lane < 5 && lane != g1 && lane != g2) S.mvalid[lane] = 0;
         const int m = rw == nldw ? g1 : g2;
         if (m >= 0) {
@@ -781,6 +779,10 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
         bool ovf = false;
         const uint64_t acc = lpc_abs2_f64<4>(xd, kF[m], 0, skip, ovf);
         if (i0 < n && acc) atomicAdd(&S.u.psum[m][pidx0], (unsigned long long)acc);
+        if (!(wv & 1)) {  // (3.7d, as in the fast FIXED sums above)
+          const uint64_t ws = wave_sum_u64_dpp(i0 < n ? acc : 0ull);
+          if (lane == 0 && ws) atomicAdd(&S.ftot_s[m], (unsigned long long)ws);
+        }
         if (__any(i0 < n && ovf) && lane == 0) S.mvalid[m] = 0;
       }
     }
@@ -826,7 +828,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
 #pragma unroll
       for (int j = 0; j < MAXO; j++) q[j] = __builtin_amdgcn_readfirstlane(S.mcoef[m][j]);
       bool ovf = false;
-      uint64_t acc = 0;
+      uint64_t acc = 0, accs = 0;  // (accs: a FIXED order's even-quarter total, 3.7d)
       if (i0 < n) {
         int pidx = pidx0, pend = (pidx + 1) * psz;
         const int iend = min(i0 + kChunk, n);
@@ -840,8 +842,10 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
           const int64_t r = gres_lds<B32, MAXO>(S.smp, i, q, sh);
           if constexpr (B32) ovf |= (r > INT32_MAX || r < INT32_MIN);
           acc += abs2_64(r);
+          if (m < 5 && !((i >> 10) & 1)) accs += abs2_64(r);
         }
         if (acc) atomicAdd(&S.u.psum[m][pidx], (unsigned long long)acc);
+        if (accs) atomicAdd(&S.ftot_s[m], (unsigned long long)accs);
       }
       if constexpr (B32) {
         if (__any(ovf) && lane == 0) S.mvalid[m] = 0;  // benign race: every writer stores 0
@@ -855,7 +859,7 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
   // ---- 5. every partition order of a model in one pass (one wave per model)
   int fg1 = -1, fg2 = -1;
   if (!early) {  // FIXED candidates (3.7): excluded orders are invalidated before the winner barrier
-    fixed_guess2(S.u.psum, S.mvalid, P, lane, fg1, fg2);
+    fixed_guess2(S.ftot_s, S.mvalid, lane, fg1, fg2);
     if (rw == 0 && lane < 5 && lane != fg1 && lane != fg2) S.mvalid[lane] = 0;
   }
   // the models left to search, dealt to the waves in order (r06: compacted, so that 2 LPC models of 6 windows

@@ -393,6 +393,9 @@ template <int MAXLAG, int PCAP, bool K17>
 #ifndef FRA_W_WAVES
 #define FRA_W_WAVES 4
 #endif
+#ifndef FRA_W_VGPR_FLOOR
+#define FRA_W_VGPR_FLOOR 1
+#endif
 #ifndef FRA_W_WAVES_MAX
 #define FRA_W_WAVES_MAX 8
 #endif
@@ -402,6 +405,12 @@ k_analyze_w(JobArgs a, int src) {
   __shared__ WaveSmem S;
   uint32_t* const sw = S.sw;
   const int lane = (int)threadIdx.x;
+#if FRA_W_VGPR_FLOOR
+  // occupancy 4 waves per SIMD by register count (r06): FRA-1 3.7d brought the kernel to 93 VGPRs, which lets a
+  // fifth wave per SIMD in and takes the room the pipelined step's background kernels co-run in (C4 step 1.374 ->
+  // 1.42 ms, C3 0.905 -> 0.96, profiles/r06_ab_fixed_sampled.txt); a clobbered v103 keeps the allocation at 104
+  asm volatile("" ::: "v103");
+#endif
   FRA_WSTAMP(0)
 #ifndef FRA_W_XCD
 #define FRA_W_XCD 1
@@ -495,8 +504,11 @@ k_analyze_w(JobArgs a, int src) {
   constexpr int npl = 6 - gsl;  // log2 finest partitions per iteration
   const int pj = lane >> npl;  // the iteration of partition `lane` (>= 4: lane >= 2^P, none)
   const int psrc = ((lane & ((1 << npl) - 1)) << gsl) | ((1 << gsl) - 1);  // its group's last lane
+  // FRA-1 3.7d (r06): the five orders' sums over the even quarters of the block only (iterations j = 0, 2: chunks
+  // 0-63 and 128-191 = samples [0, 1024) and [2048, 3072)) choose the two candidates; their sums over iterations 1
+  // and 3 follow for those two orders alone (pass B below)
   uint32_t pfix[5] = {0, 0, 0, 0, 0};
-  for (int j = 0; j < kWIters; j++) {
+  for (int j = 0; j < kWIters; j += 2) {
     const int t = 64 * j + lane;
     const bool head = t == 0;
     uint32_t D[14];
@@ -551,6 +563,42 @@ k_analyze_w(JobArgs a, int src) {
   for (int k = 0; k < 5; k++) {
     pf1 = k == g1 ? pfix[k] : pf1;
     pf2 = k == g2 ? pfix[k] : pf2;
+  }
+  // pass B (3.7d): orders g1 and g2 over iterations 1 and 3 (the odd quarters), the same difference chain and SADs
+  {
+    const int kmax = g1 > g2 ? g1 : g2;  // (uniform)
+#pragma unroll 1
+    for (int j = 1; j < kWIters; j += 2) {
+      uint32_t D[14];
+      wread_d14(sw, lane, j, D);
+      int32_t x[28];
+      unpack28(D, x);
+      uint32_t v[28];
+#pragma unroll
+      for (int jx = 8; jx < 28; jx++) v[jx] = (uint32_t)x[jx] ^ kBias;
+      uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+      for (int k = 0; k <= 4; k++) {
+        if (k > kmax) break;  // (uniform)
+        if (k > 1) {
+#pragma unroll
+          for (int jx = 12 + kChunk - 1; jx >= 7 + k; jx--) v[jx] = xad_bias(v[jx - 1], v[jx]);
+        }
+        if (k == g1 || k == g2) {  // (uniform; no warm-up positions here: chunk 64 j + lane > 0)
+          uint32_t s32 = 0;
+#pragma unroll
+          for (int jj = 0; jj < kChunk; jj++) s32 = sad_acc(v[12 + jj], k == 0 ? kBias : v[11 + jj], s32);
+          if (k == g1) s1 = s32;
+          else s2 = s32;
+        }
+      }
+      const uint32_t gs1 = bperm32(group_sum32(s1, gsl), psrc), gs2 = bperm32(group_sum32(s2, gsl), psrc);
+      pf1 = pj == j ? 2u * gs1 : pf1;
+      pf2 = pj == j ? 2u * gs2 : pf2;
+    }
+    // the two candidates' FULL block totals, for the gate (3.7c)
+    gt1 = (uint64_t)wave_sum32(pf1);
+    gt2 = (uint64_t)wave_sum32(pf2);
   }
 #if defined(FRA_WPAD) && FRA_WPAD > 0
   {  // diagnostic build only (tools/gpu_r04_pad.sh): FRA_WPAD extra independent VALU instructions per wave

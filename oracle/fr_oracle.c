@@ -362,7 +362,8 @@ static int best_order_by_error(const double *err, int norders, int n, int overhe
 
 /* FRA-1 3.7b override (tests / size studies only): < 0 = the level table's lpc_keep, 0 = every window, k = k */
 static int ora_lpc_keep = -1;
-/* FRA-1 3.7c override (tests / size studies only): 1 = every FIXED candidate is searched (pre-r06 rule) */
+/* FRA-1 3.7c/3.7d override (tests / size studies only): 1 = the pre-r06 FIXED rule (candidates chosen on full
+ * block totals, every candidate searched) */
 static int ora_fixed_all = 0;
 ORA_API void ora_set_fixed_all(int on) { ora_fixed_all = on != 0; }
 ORA_API void ora_set_lpc_keep(int k) { ora_lpc_keep = k; }
@@ -560,11 +561,18 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
     uint64_t bt1 = 0, bt2 = 0;
     for (int o = 0; o <= fmax; o++) {
       if (!compute_residual(s, n, 2, o, NULL, 0, r)) continue;
-      uint64_t T = 0;
-      for (int i = o; i < n; i++) T += 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
+      /* 3.7d (r06): the candidates are chosen on the totals over the even 1024-sample quarters of the block,
+       * samples i with (i >> 10) even (half the FIXED sums work on the GPU); the gate (3.7c) uses full totals */
+      uint64_t T = 0, Ts = 0;
+      for (int i = o; i < n; i++) {
+        const uint64_t a2 = 2 * (uint64_t)(r[i] < 0 ? -r[i] : r[i]);
+        T += a2;
+        if (!((i >> 10) & 1)) Ts += a2;
+      }
       fT[o] = T;
-      if (fg1 < 0 || T < bt1) { bt2 = bt1; fg2 = fg1; bt1 = T; fg1 = o; }
-      else if (fg2 < 0 || T < bt2) { bt2 = T; fg2 = o; }
+      const uint64_t Tsel = ora_fixed_all ? T : Ts;
+      if (fg1 < 0 || Tsel < bt1) { bt2 = bt1; fg2 = fg1; bt1 = Tsel; fg1 = o; }
+      else if (fg2 < 0 || Tsel < bt2) { bt2 = Tsel; fg2 = o; }
     }
   }
   uint64_t lpcT = UINT64_MAX; /* smallest block total of 2|r| over the LPC models evaluated (3.7c) */
