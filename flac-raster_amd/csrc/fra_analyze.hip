@@ -594,6 +594,9 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
       // 3.1 autocorrelation of every window: windowed samples -> chunk partials -> wave
       // reduce-scatter -> red[wi][wave][lag].  Window 0 is peeled so its prefetched coefficients die
       // at their first use.
+      // FRA-1 3.5b: the 16-bit instance's subframes (streams of <= 16 bps) sum integers; the 32-bit instance --
+      // 32-bps streams and the mid / side virtual channels of 16-bps stereo -- keeps 3.4's float chunk sums
+      constexpr bool irule = !B32;
       auto window_acf = [&](const int wi, const bool act) {
         if (!act) {
           if (lane <= MAXLAG) S.red()[wi][wv][lane] = 0.0;  // = the all-zero partials (+0.0 exactly)
@@ -620,6 +623,24 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
           }
         }
 
+        double acc[MAXLAG + 1];
+        if constexpr (irule) {
+          // FRA-1 3.5b (the 16-bit instance): the windowed samples rounded to integers (|v| <= 2^15) and their
+          // products summed as doubles -- exact (chunk partials < 2^35, totals < 2^43), so the reduction order
+          // below does not matter; samples at or past n have 0.0f coefficients: v = 0
+          double dv[kChunk + MAXLAG];
+#pragma unroll
+          for (int j = 0; j < kChunk + MAXLAG; j++) dv[j] = (double)__builtin_rintf(wf[j]);
+#pragma unroll
+          for (int l = 0; l <= MAXLAG; l++) {
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < kChunk; j++) s = fma(dv[j], dv[j + l], s);
+            acc[l] = s;
+          }
+          autocorr_reduce_wave<MAXLAG + 1>(acc, S.red()[wi][wv], lane);
+          return;
+        }
         // chunk partials (FRA-1): per lag, the even and the odd samples of the chunk are summed
         // separately in float (fused multiply-add, ascending), then ae + ao in float, widened to double
         // -- one v_pk_fma_f32 per (sample pair, lag).  Samples at or past n are 0.0f, whose products
@@ -636,7 +657,6 @@ __global__ void __launch_bounds__(kThreads, B32 ? 5 : (MAXLAG > 8 ? 4 : kWaves16
             pacc[l] = __builtin_elementwise_fma(a2, b2, pacc[l]);
           }
         }
-        double acc[MAXLAG + 1];
 #pragma unroll
         for (int l = 0; l <= MAXLAG; l++) acc[l] = (double)(pacc[l].x + pacc[l].y);
         autocorr_reduce_wave<MAXLAG + 1>(acc, S.red()[wi][wv], lane);

@@ -39,6 +39,7 @@ constexpr int kWIters = kWChunks / 64;        // chunks per lane
 // [8t, 8t + 8).  The bit buffer aliases them (<= 2,047 words + one spare; a longer subframe takes the sample path)
 struct WaveSmem {
   uint32_t sw[8 * kWChunks];
+  double acf[3][9];  // FRA-1 3.5b: each window's autocorrelation (lags 0..8), read back per lane group
 };
 constexpr uint32_t kBufWords = 8 * kWChunks;
 
@@ -393,6 +394,9 @@ template <int MAXLAG, int PCAP, bool K17>
 #ifndef FRA_W_WAVES
 #define FRA_W_WAVES 4
 #endif
+#ifndef FRA_W_ACF_ITERS  // diagnostic builds only: autocorrelation over the first k 1024-sample iterations
+#define FRA_W_ACF_ITERS 4
+#endif
 #ifndef FRA_W_VGPR_FLOOR
 #define FRA_W_VGPR_FLOOR 1
 #endif
@@ -627,99 +631,120 @@ k_analyze_w(JobArgs a, int src) {
     if (cfg.nsub > 0 && lmax > 0) {
       nlpc = a.nwin;
       const int nwin = a.nwin;
-      constexpr int NL = MAXLAG + 1, N16 = ((NL + 1) / 2 + 1) / 2;
+      constexpr int NL = MAXLAG + 1;
       double acl[NL];
-#pragma unroll
-      for (int l = 0; l < NL; l++) acl[l] = 0.0;
       for (int wi = 0; wi < nwin; wi++) {
         const int32_t* wr = a.wrange + 2 * ((size_t)wd.win * a.nwin + wi);
         const int32_t* wp = a.wplat + 2 * ((size_t)wd.win * a.nwin + wi);
         const int lo = wr[0], hi = wr[1], plo = wp[0], phi = wp[1];
         const float* win = a.win + ((size_t)wd.win * a.nwin + wi) * a.blocksize;
-        double s01[N16], s[N16];
+        // FRA-1 3.5b on the matrix cores.  The windowed integer samples v (|v| < 2^15) as a 256 x 16 matrix
+        // Y[k][i] = v[16 k + i] (k = 16 g + e per 1024-sample block: lane 16 g + i holds rows k of its group in
+        // its 16 bytes, e = 0..15, and the next row k + 1 for the shifted copy): C0 = Y^T Y and C1 = Y^T Y'
+        // (Y' = the rows one down) give R[L] = sum_{i <= 15-L} C0[i][i+L] + sum_{i >= 16-L} C1[i][i+L-16].
+        // Each v = 256 h + (l + 128) with h = v >> 8 and l = (v & 255) - 128 signed bytes, the products
+        // h h', h l' + l h', l l' accumulated exactly in int32 by v_mfma_i32_16x16x64_i8 (|sums| < 2^23), and
+        // R[L] = 65536 HH + 256 HL + LL + 256 sum(v) - 128 sum_{m<L} v[m] - 2^26 (the offsets of the 4,096
+        // pairs, samples past n being v = 0) -- exact, like the oracle's int64 sums
+        const int ri = lane & 15, g4 = lane >> 4;
+        i32x4 c0h = {0, 0, 0, 0}, c0m = c0h, c0l = c0h, c1h = c0h, c1m = c0h, c1l = c0h;
+        int32_t ysh = 0, ysl = 0, yfirst = 0;  // sums of the samples' h and l bytes; sample of lane ri (< 16)
+        const int16_t* const sh16 = reinterpret_cast<const int16_t*>(sw);
+        for (int blk = 0; blk < kWIters; blk++) {
+          const int b0 = 1024 * blk;
+          // elements 0..15: samples b0 + 256 g4 + 16 e + ri; element 16: the next row (past n: 0).  The lane's
+          // offset is opaque per block, so the per-element addresses stay immediate offsets of one base instead
+          // of 17 x 4 hoisted 64-bit addresses (which spilled)
+          int sb = b0 + 256 * g4 + ri;
+          asm volatile("" : "+v"(sb));
+          const int16_t* const sp = sh16 + sb;
+          const float* const wp = win + sb;
+          const int kind = (!(lo < b0 + 1024 && hi > b0) || blk >= FRA_W_ACF_ITERS) ? 0
+                           : (b0 >= plo && b0 + 1024 <= phi) ? 1 : 2;  // zero / plateau (1.0f) / windowed
+          uint32_t H[5], L[5];
+          // two halves of 8 elements, loaded, windowed and packed in turn (all 16 in flight at once needed
+          // more than the kernel's 104 VGPRs)
 #pragma unroll
-        for (int k = 0; k < N16; k++) { s01[k] = 0.0; s[k] = 0.0; }
-        // the lane's addresses are recomputed per window (opaque lane): hoisted out of the window loop
-        // they would stay live across it and cost registers the rest of the kernel needs
-        int lnw = lane;
-        asm volatile("" : "+v"(lnw));
-        for (int j = 0; j < kWIters; j++) {
-          double z[N16];
-          // an iteration whose samples + look-ahead miss the window's nonzero extent sums exact zeros:
-          // every chunk partial is +0.0 (k_analyze's inactive wave)
-          if (lo < 1024 * j + 1024 + MAXLAG && hi > 1024 * j) {
-            const int t = 64 * j + lnw, i0 = kChunk * t;
-            // samples 16t .. 16t + 15 + MAXLAG: the chunk and the next one's first 8 (the last chunk's
-            // look-ahead re-reads itself: those samples meet 0.0f coefficients past n)
-            int32_t y[kChunk + MAXLAG];
-            {
-              const uint32_t* po = sw + 8 * lnw + kWIterDw * j;
-              const uint4 v0 = lds4(po), v1 = lds4(po + 4), v2 = lds4(t == kWChunks - 1 ? po : po + 8);
-              // the last chunk's look-ahead (samples past n) is zero: its coefficients may then be read without
-              // a bound (the table has slack past its last row, plan_build), and every product is still +-0
-              const bool last = t == kWChunks - 1;
-              const uint32_t dw[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                                       last ? 0u : v2.x, last ? 0u : v2.y, last ? 0u : v2.z, last ? 0u : v2.w};
+          for (int hf = 0; hf < 2; hf++) {
+            int32_t y[8];
+            if (kind == 0) {
 #pragma unroll
-              for (int p = 0; p < (kChunk + MAXLAG) / 2; p++) {
-                y[2 * p] = lo16(dw[p]);
-                y[2 * p + 1] = hi16(dw[p]);
-              }
-            }
-            // coefficients exactly 1.0f inside the plateau: the product is the sample itself (no load, and
-            // no multiply when the whole iteration lies inside); else loaded, entries at or past n 0.0f
-            const bool plat = i0 >= plo && i0 + kChunk + MAXLAG <= phi;
-            float wf[kChunk + MAXLAG];
-            if (__all(plat)) {
+              for (int e = 0; e < 8; e++) y[e] = 0;
+            } else if (kind == 1) {
 #pragma unroll
-              for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = (float)y[jx];
+              for (int e = 0; e < 8; e++) y[e] = sp[16 * (8 * hf + e)];
             } else {
-              float wc[kChunk + MAXLAG];
-              if (plat) {
+              float wc[8];
 #pragma unroll
-                for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = 1.0f;
-              } else {
+              for (int e = 0; e < 8; e++) wc[e] = wp[16 * (8 * hf + e)];
 #pragma unroll
-                for (int jx = 0; jx < kChunk + MAXLAG; jx++) wc[jx] = win[i0 + jx];  // (no per-entry bound)
-              }
-#pragma unroll
-              for (int jx = 0; jx < kChunk + MAXLAG; jx++) wf[jx] = (float)y[jx] * wc[jx];
+              for (int e = 0; e < 8; e++) y[e] = (int32_t)__builtin_rintf((float)sp[16 * (8 * hf + e)] * wc[e]);
             }
-            f32x2 pacc[NL];
+            if (blk == 0 && hf == 0) yfirst = y[0];
 #pragma unroll
-            for (int l = 0; l < NL; l++) pacc[l] = f32x2{0.0f, 0.0f};
-#pragma unroll
-            for (int pp = 0; pp < kChunk / 2; pp++) {
-              const f32x2 a2 = {wf[2 * pp], wf[2 * pp + 1]};
-#pragma unroll
-              for (int l = 0; l < NL; l++) {
-                const f32x2 b2 = {wf[2 * pp + l], wf[2 * pp + l + 1]};
-                pacc[l] = __builtin_elementwise_fma(a2, b2, pacc[l]);
-              }
+            for (int dd = 0; dd < 2; dd++) {
+              const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)y[4 * dd + 1], (uint32_t)y[4 * dd], 0x05010400u);
+              const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)y[4 * dd + 3], (uint32_t)y[4 * dd + 2], 0x05010400u);
+              L[2 * hf + dd] = __builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u;
+              H[2 * hf + dd] = __builtin_amdgcn_perm(p23, p01, 0x07060302u);
+              // sum(v) from the bytes (v = 256 h + l + 128): no sample stays live past its packing
+              ysh = __builtin_amdgcn_sdot4((int)H[2 * hf + dd], 0x01010101, ysh, false);
+              ysl = __builtin_amdgcn_sdot4((int)L[2 * hf + dd], 0x01010101, ysl, false);
             }
-            double acc[NL];
-#pragma unroll
-            for (int l = 0; l < NL; l++) acc[l] = (double)(pacc[l].x + pacc[l].y);
-            autocorr_reduce_regs<NL>(acc, z);
-          } else {
-#pragma unroll
-            for (int k = 0; k < N16; k++) z[k] = 0.0;
+            if (hf == 0) asm volatile("" ::: "memory");
           }
-          // (G0 + G1) + (G2 + G3) per lag, the order of k_analyze's cross-wave sum
-          if (j == 2) {
-#pragma unroll
-            for (int k = 0; k < N16; k++) s01[k] = s[k];
+          int32_t y16;
+          {
+            const bool in = blk < kWIters - 1 || g4 < 3;  // the next row lies inside the block of n samples
+            const float x16 = in ? (float)sp[256] : 0.0f;
+            y16 = (int32_t)__builtin_rintf(x16 * (in ? wp[256] : 0.0f));
           }
-#pragma unroll
-          for (int k = 0; k < N16; k++) s[k] = (j & 1) ? s[k] + z[k] : z[k];
+          H[4] = (uint32_t)y16 >> 8;
+          L[4] = (uint32_t)y16 ^ 0x80u;
+          const i32x4 xh = {(int)H[0], (int)H[1], (int)H[2], (int)H[3]};
+          const i32x4 xl = {(int)L[0], (int)L[1], (int)L[2], (int)L[3]};
+          const i32x4 sh = {(int)__builtin_amdgcn_alignbyte(H[1], H[0], 1), (int)__builtin_amdgcn_alignbyte(H[2], H[1], 1),
+                            (int)__builtin_amdgcn_alignbyte(H[3], H[2], 1), (int)__builtin_amdgcn_alignbyte(H[4], H[3], 1)};
+          const i32x4 sl = {(int)__builtin_amdgcn_alignbyte(L[1], L[0], 1), (int)__builtin_amdgcn_alignbyte(L[2], L[1], 1),
+                            (int)__builtin_amdgcn_alignbyte(L[3], L[2], 1), (int)__builtin_amdgcn_alignbyte(L[4], L[3], 1)};
+          c0h = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, xh, c0h, 0, 0, 0);
+          c0m = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, xl, c0m, 0, 0, 0);
+          c0m = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, xh, c0m, 0, 0, 0);
+          c0l = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, xl, c0l, 0, 0, 0);
+          c1h = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, sh, c1h, 0, 0, 0);
+          c1m = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, sl, c1m, 0, 0, 0);
+          c1m = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, sh, c1m, 0, 0, 0);
+          c1l = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, sl, c1l, 0, 0, 0);
         }
-        const int gw = lane >> 4;
+        // C element (row 4 g4 + q, column ri) at lane 16 g4 + ri, register q: lag (ri - 4 g4 - q) mod 16, from C0
+        // when ri >= row, else C1; rotated within the row so that lane 16 g4 + L holds lag L, rows summed
+        double mq = 0.0;
 #pragma unroll
-        for (int l = 0; l < NL; l++) {
-          const int sl = lag_slot<NL>(l);
-          const double tot = rdlane_f64(s01[sl >> 2] + s[sl >> 2], 16 * (sl & 3) + 15);
-          acl[l] = gw == wi ? tot : acl[l];
+        for (int q = 0; q < 4; q++) {
+          const int dd = ri - 4 * g4 - q;
+          const bool in0 = dd >= 0;
+          const double v = fma((double)(in0 ? c0h[q] : c1h[q]), 65536.0,
+                               fma((double)(in0 ? c0m[q] : c1m[q]), 256.0, (double)(in0 ? c0l[q] : c1l[q])));
+          mq = mq + __shfl(v, 16 * g4 + ((ri + 4 * g4 + q) & 15), 64);
         }
+        mq = mq + __shfl_xor(mq, 16, 64);
+        mq = mq + __shfl_xor(mq, 32, 64);
+        const int32_t ytot = (int32_t)wave_sum32((uint32_t)(256 * ysh + ysl)) + 128 * kMaxBlock;
+        int32_t pre = 0;  // sum of v[m], m < L, at lane L (samples 0..7: lanes 0..7, block 0, element 0)
+#pragma unroll
+        for (int m = 0; m < MAXLAG; m++) {
+          const int32_t vm = __builtin_amdgcn_readlane(yfirst, m);
+          pre += ri > m ? vm : 0;
+        }
+        const double rl = mq + (256.0 * (double)ytot - 128.0 * (double)pre - 67108864.0);
+        if (lane < NL) S.acf[wi][lane] = rl;  // (through LDS: nine doubles per lane kept live across the
+                                              // windows would push the phase past 128 VGPRs)
+      }
+      wsync();
+      {
+        const int gw = min(lane >> 4, nwin - 1);
+#pragma unroll
+        for (int l = 0; l < NL; l++) acl[l] = S.acf[gw][l];
       }
       FRA_WSTAMP(4)
 #ifdef FRA_WSTOP

@@ -112,6 +112,7 @@ template <> struct RawType<ST_F32> { using T = float; };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));  // a 16x16 int32 MFMA tile / 16 int8 MFMA operands
 
 // normalisation-table index of a <= 16-bit integer raster value: its bit pattern as an unsigned integer
 // (k_norm_lut fills the entries of the tile's values mn..mx)

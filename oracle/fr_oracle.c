@@ -257,6 +257,19 @@ ORA_API void ora_autocorr(const float *wf, int n, int maxlag, double *autoc) {
   }
 }
 
+/* FRA-1 3.5b (r06): integer autocorrelation for the coded channels of streams of <= 16 bps.  The windowed
+ * sample is the integer v[i] = rint((float)s[i] * w[i]) (the float product of 3.4, rounded half to even), and
+ * R[l] = sum_{i < n-l} v[i] v[i+l] is exact (|v| <= 2^15, n <= 4096: |R| < 2^43), so no summation order is
+ * part of the rule -- the GPU sums it on the matrix cores (k_analyze_w) or as exact doubles (k_analyze). */
+ORA_API void ora_autocorr_int(const int32_t *v, int n, int maxlag, double *autoc) {
+  for (int l = 0; l <= maxlag; l++) {
+    int64_t acc = 0;
+    for (int i = 0; i + l < n; i++) acc += (int64_t)v[i] * v[i + l];
+    autoc[l] = (double)acc;
+  }
+}
+ORA_API int32_t ora_window_int(int32_t s, float w) { return (int32_t)rintf((float)s * w); }
+
 /* Levinson-Durbin.  lp[o-1][j], j<o = predictor coefficients for order o,
  * err[o-1] = prediction error.  Returns the number of valid orders (stops when err <= 0). */
 ORA_API int ora_levinson(const double *autoc, int max_order, double *lp /* max_order*32 */, double *err_out) {
@@ -520,7 +533,7 @@ typedef struct {
 
 /* Encode decision for one subframe. s = channel samples (int64), n = block. */
 static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cfg *cfg, const winset_t *ws,
-                             sf_t *d, int64_t *s, int64_t *r, int64_t *rbest, float *wf) {
+                             sf_t *d, int64_t *s, int64_t *r, int64_t *rbest, float *wf, int irule) {
   memset(d, 0, sizeof(*d));
   /* 3.2 constant */
   int allsame = 1;
@@ -587,9 +600,15 @@ static void analyze_subframe(const int64_t *s_in, int n, int bps, const level_cf
     double scw[MAXW];
     for (int wi = 0; wi < ws->nwin; wi++) {
       const float *win = ws->win + (size_t)wi * n;
-      for (int i = 0; i < n; i++) wf[i] = (float)s[i] * win[i];
       double autoc[33];
-      ora_autocorr(wf, n, lmax, autoc);
+      if (irule) { /* 3.5b: integer windowed samples, exact autocorrelation */
+        int32_t *wv = (int32_t *)wf;
+        for (int i = 0; i < n; i++) wv[i] = (int32_t)rintf((float)s[i] * win[i]);
+        ora_autocorr_int(wv, n, lmax, autoc);
+      } else {
+        for (int i = 0; i < n; i++) wf[i] = (float)s[i] * win[i];
+        ora_autocorr(wf, n, lmax, autoc);
+      }
       okw[wi] = 0;
       if (!(autoc[0] != 0.0)) continue;
       double lp[32 * 32], err[32];
@@ -853,7 +872,11 @@ static void encode_frames(bw_t *bw, const int32_t *x, int64_t N, int C, int bps,
         else s_in[i] = l - rr;
       }
       if (ms && c == 3) cb = bps + 1;  /* the side channel */
-      analyze_subframe(s_in, n, cb, cfg, &ws, &d[c], sh + (size_t)c * blocksize, r, rb + (size_t)c * blocksize, wf);
+      /* FRA-1 3.5b: the coded channels of streams of <= 16 bps sum integers; 32-bps streams and the mid / side
+       * virtual channels (GPU: the 32-bit k_analyze instance) keep 3.4's float chunk sums */
+      const int irule = bps <= 16 && !(ms && c >= 2);
+      analyze_subframe(s_in, n, cb, cfg, &ws, &d[c], sh + (size_t)c * blocksize, r, rb + (size_t)c * blocksize, wf,
+                       irule);
       if (d[c].type == 0) { /* constant: analysis returned before filling the shifted copy */
         for (int i = 0; i < n; i++) sh[(size_t)c * blocksize + i] = s_in[i];
       }

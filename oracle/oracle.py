@@ -67,6 +67,7 @@ def lib():
     L.ora_window_set.argtypes = [p, C.c_int, C.c_int]
     L.ora_num_windows.argtypes = [C.c_int]
     L.ora_autocorr.argtypes = [p, C.c_int, C.c_int, p]
+    L.ora_autocorr_int.argtypes = [p, C.c_int, C.c_int, p]
     L.ora_levinson.argtypes = [p, C.c_int, p, p]
     L.ora_quantize.argtypes = [p, C.c_int, C.c_int, p, C.POINTER(C.c_int)]
     L.ora_det_log2.argtypes = [C.c_double]
@@ -184,6 +185,14 @@ def autocorr(wf: np.ndarray, maxlag: int) -> np.ndarray:
     a = np.ascontiguousarray(wf, dtype=np.float32)
     out = np.zeros(maxlag + 1, dtype=np.float64)
     lib().ora_autocorr(_ptr(a), a.size, maxlag, _ptr(out))
+    return out
+
+
+def autocorr_int(v: np.ndarray, maxlag: int) -> np.ndarray:
+    """FRA-1 3.5b: exact autocorrelation of integer windowed samples (streams of <= 16 bps)."""
+    a = np.ascontiguousarray(v, dtype=np.int32)
+    out = np.zeros(maxlag + 1, dtype=np.float64)
+    lib().ora_autocorr_int(_ptr(a), a.size, maxlag, _ptr(out))
     return out
 
 

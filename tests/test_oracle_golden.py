@@ -135,6 +135,12 @@ def test_window_and_lpc_primitives():
     x = np.cumsum(rng.normal(size=4096)).astype(np.float32)
     ac = O.autocorr(x, 8)
     assert ac[0] > 0 and np.all(np.abs(ac[1:]) <= ac[0])
+    # FRA-1 3.5b: integer windowed samples, exact sums (= numpy int64), extremes included
+    v = np.clip(np.rint(x * 3000.0), -32768, 32767).astype(np.int32)
+    v[:3] = [-32768, 32767, -32768]
+    ai = O.autocorr_int(v, 8)
+    ref = [int(np.dot(v[: 4096 - l].astype(np.int64), v[l:].astype(np.int64))) for l in range(9)]
+    assert [int(t) for t in ai] == ref and ai.dtype == np.float64
     lp, err, n = O.levinson(ac, 8)
     assert n == 8 and np.all(np.diff(err) <= 0)
     q, sh = O.quantize(lp[1], 2, 12)
