@@ -58,8 +58,10 @@ def frames_of(tile: Tuple[int, int, int, int], blocksize: int = 4096) -> int:
 # What holding partial last frames (n < blocksize) costs a rank, in full frames: those subframes run as ONE separate,
 # latency-bound k_analyze launch per execute beside the per-wave analysis of the full frames, whatever their number.
 # Measured on the C4 8-way split (r06, profiles/r06_shards_partial_cost.txt): the one rank holding the scene's only
-# partial frame (the 740^2 corner tile) stepped ~0.012 ms (~6 %, about 240 frames of analysis) slower than the others.
-PARTIAL_FRAME_COST = 256
+# partial frame (the 740^2 corner tile) stepped ~0.012 ms (~6 %, about 240 frames of analysis) slower than the others;
+# after FRA-1 3.5b made the frames cheaper the same launch weighs ~500 frames (256 -> 512: slowest 8-way share 0.200 ->
+# 0.190 ms, profiles/r06_shards_final.txt).
+PARTIAL_FRAME_COST = 512
 
 
 def frame_split(tiles: Sequence[Tuple[int, int, int, int]], parts: int,

@@ -38,7 +38,8 @@ shard = os.environ.get("SHARD")  # R/N: rank R's frame-split share (bench.py --s
 if shard:
     from flac_raster.tiles import frame_split
     sr, sn = (int(x) for x in shard.split("/"))
-    items = frame_split(wins, sn)[sr]
+    pc = os.environ.get("SHARD_COST")  # partial_cost override (tiles.PARTIAL_FRAME_COST)
+    items = (frame_split(wins, sn, partial_cost=int(pc)) if pc else frame_split(wins, sn))[sr]
     wins = [wins[i] for i, _, _ in items]
     ranges = [(f0, n) for _, f0, n in items]
 plan = N.Plan(ctx, dev, True, dt, B, (H * W, W, 1), wins, cfg["level"], 4096, cfg["norm"], frame_ranges=ranges)
