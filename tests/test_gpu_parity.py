@@ -380,3 +380,24 @@ def test_wave_kernel_constant_and_two_valued(require_wave):
     x[0, 64:128] = 1234
     x[0, 128:] = np.where(base % 2 == 0, -5, 7).astype(np.int16)
     check_windows(x, [(0, 0, 64, 192), (64, 0, 64, 192), (128, 0, 64, 192), (0, 0, 192, 192)], 5, 16)
+
+
+@pytest.mark.parametrize("level", [3, 5, 6])
+def test_integer_autocorrelation_full_scale(level):
+    """FRA-1 3.5b at the int16 extremes (pyflac path, pre-normalised audio): full-scale square waves (-32768 /
+    32767: signed high bytes -128 / 127, low bytes 0 / 255), a full-range ramp and a slow sine with the extremes
+    in the plateau and the tapers of the windows (level 6: the two partial tukeys, zero blocks of the matrix-core
+    sums), 4,096-sample frames plus a partial last frame."""
+    n = 4096 * 6 + 1000
+    i = np.arange(n)
+    sq = np.where((i // 37) % 2 == 0, -32768, 32767)
+    ramp = ((i * 16) % 65536) - 32768
+    sine = np.round(32767 * np.sin(i / 300.0))
+    mix = np.where(i < n // 2, sq, sine)
+    for sig in (sq, ramp, sine, mix):
+        audio = sig.astype(np.int16).reshape(-1, 1)
+        _, frames = N.encode_interleaved(audio, 44100, level=level)
+        assert frames == O.encode(audio, 44100, level=level, with_header=False)
+    stereo = np.stack([sq, sine], axis=1).astype(np.int16)  # two channels: mid / side at levels 5-6
+    _, frames = N.encode_interleaved(stereo, 44100, level=level)
+    assert frames == O.encode(stereo, 44100, level=level, with_header=False)
