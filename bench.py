@@ -10,7 +10,8 @@ in HBM (the bytes the reference's pyflac/libFLAC calls produce per tile, cli.py:
 
 Multi-GPU (one process per GPU): under torch.distributed.run, or ``--gpus N`` alone, which starts the N rank
 processes itself before touching the GPU.  STRONG scaling by default -- BASELINE's C4/C5 are ONE scene split
-over the GPUs into (tile, frame range) items of equal frame count (``--split frames``), no
+over the GPUs into (tile, frame range) items of equal cost (``--split frames``: frames, plus a fixed charge for
+partial frames), no
 collective on the data path; ``value`` = scene pixels / max-over-ranks time; per-rank times and the imbalance
 are reported.  ``--scaling weak`` instead gives every rank its own scene (seed + rank).
 
@@ -463,7 +464,7 @@ def main():
                     help="time rank R's share (--split) of the scene for an N-GPU strong-scaling run, on this one GPU "
                          "(projection of the multi-GPU step; DESIGN.md section 7)")
     ap.add_argument("--split", default="frames", choices=["frames", "strided", "lpt"],
-                    help="strong scaling: (tile, frame range) work items of equal frame count per rank (default; "
+                    help="strong scaling: (tile, frame range) work items of equal cost per rank (default; "
                          "fra_plan_create_ranged), the same over the tiles in strided order, or whole tiles by LPT")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 counter passes")
@@ -772,7 +773,8 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "u16->i16 (int32 analysis, f32 chunk partials + f64 autocorr tree)" if cfg["norm"] == 16 else "f32->i32 (int64 analysis)",
+            "dtype": ("u16->i16 (int32 analysis, exact integer autocorrelation on i8 MFMA)" if cfg["norm"] == 16
+                      else "f32->i32 (int64 analysis, f32 chunk partials + f64 autocorrelation tree)"),
             "data": "synthetic (flac_raster.synth, seed 20260227; device-generated, integer-exact numpy mirror)",
             "config": {"workload": cfg["workload"], "level": cfg["level"], "tiles": len(wins),
                        "raster_bytes": raster_bytes, "compressed_bytes": int(out_bytes_all),
@@ -780,8 +782,8 @@ def main():
                        "msamples_per_s": round(job_px * B * args.steps / T / 1e6, 1),
                        "parallelism": (f"{world} scene(s), one per GPU, no collective" if weak else
                                        "one scene over {} GPU(s), no collective: {}".format(world, {
-                                           "frames": "(tile, frame range) items of equal frame count per rank",
-                                           "strided": "(tile, frame range) items of equal frame count per rank, "
+                                           "frames": "(tile, frame range) items of equal cost per rank (frames + partial-frame charge)",
+                                           "strided": "(tile, frame range) items of equal cost per rank, "
                                                       "tiles in strided order",
                                            "lpt": "whole tiles by LPT on pixel count"}[args.split])),
                        "split": args.split,
