@@ -39,7 +39,7 @@ constexpr int kWIters = kWChunks / 64;        // chunks per lane
 // [8t, 8t + 8).  The bit buffer aliases them (<= 2,047 words + one spare; a longer subframe takes the sample path)
 struct WaveSmem {
   uint32_t sw[8 * kWChunks];
-  double acf[3][9];  // FRA-1 3.5b: each window's autocorrelation (lags 0..8), read back per lane group
+  double acf[3][9];      // FRA-1 3.5b: each window's autocorrelation (lags 0..8), read back per lane group
 };
 constexpr uint32_t kBufWords = 8 * kWChunks;
 
@@ -111,41 +111,6 @@ __device__ __forceinline__ double rdlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// autocorr_reduce_wave (fra_device.h) without the store: the same reduce-scatter, the lag sums left in
-// z[k] at lanes 16r + 15; kLagK / kLagR say where lag L ends up
-template <int NL>
-__device__ __forceinline__ void autocorr_reduce_regs(const double (&acc)[NL], double (&z)[((NL + 1) / 2 + 1) / 2]) {
-  constexpr int N32 = (NL + 1) / 2, N16 = (N32 + 1) / 2;
-  double w[N32];
-#pragma unroll
-  for (int k = 0; k < N32; k++) {
-    double x = acc[2 * k], y = (2 * k + 1 < NL) ? acc[2 * k + 1] : acc[2 * k];
-    swap32_f64(x, y);
-    w[k] = x + y;
-  }
-#pragma unroll
-  for (int k = 0; k < N16; k++) {
-    double x = w[2 * k], y = (2 * k + 1 < N32) ? w[2 * k + 1] : w[2 * k];
-    swap16_f64(x, y);
-    double v = x + y;
-    v = v + dppf64<DPP_SHR8, 0xF>(v);
-    v = v + dppf64<DPP_SHR4, 0xF>(v);
-    v = v + dppf64<DPP_SHR2, 0xF>(v);
-    v = v + dppf64<DPP_SHR1, 0xF>(v);
-    z[k] = v;
-  }
-}
-template <int NL>
-__host__ __device__ constexpr int lag_slot(int lag) {  // (k << 2) | r of the first slot holding lag
-  constexpr int N32 = (NL + 1) / 2, N16 = (N32 + 1) / 2;
-  for (int k = 0; k < N16; k++)
-    for (int r = 0; r < 4; r++) {
-      const int wi = (2 * k + 1 < N32) ? 2 * k + (r & 1) : 2 * k;
-      const int l = (2 * wi + 1 < NL) ? 2 * wi + (r >> 1) : 2 * wi;
-      if (l == lag) return (k << 2) | r;
-    }
-  return -1;
-}
 
 // Levinson-Durbin (op sequence of levinson_wave / oracle ora_levinson) where each lane keeps only what its
 // order lo needs: the prediction error after step lo - 1 (e, step 0's for lo = 0) and that step's row,
